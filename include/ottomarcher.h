@@ -1,0 +1,197 @@
+/*
+ * ottomarcher.h — C-ABI of the MI355X-native path-tracing hot path
+ * (drop-in for octaviogarcia/RaytracingOneWeekend's per-pixel ray_color path).
+ *
+ * Every entry point is extern "C", takes plain pointers/sizes, never unwinds,
+ * and returns om_status (0 = OK, negative = error; om_last_error() explains).
+ * No torch or HIP types appear in the signatures.
+ *
+ * Reference interfaces replaced (file:line under /root/reference/src/):
+ *   om_world_*            HittableList::new / += &T / clear         hits.rs:71-110, 370-371
+ *   om_world_add_sphere   Sphere::new                               traced.rs:22-25
+ *   om_world_add_sphere_radius  Sphere::new_with_radius             traced.rs:26-31
+ *   om_world_add_cube     Cube::new                                 traced.rs:238-240
+ *   om_world_add_cube_length    Cube::new_with_length               traced.rs:242-246
+ *   om_world_add_triangle / _parallelogram  Barycentric::new3points traced.rs:148-154
+ *   om_world_add_triangle_basis / _parallelogram_basis  Barycentric::new  traced.rs:135-147
+ *   om_world_add_plane    InfinitePlane::new                        traced.rs:86-88
+ *   om_world_add_marched_sphere / _box   struct literals            marched.rs:50-54, 79-83
+ *   om_world_add_marched_torus  MarchedTorus::new                   marched.rs:116-130
+ *   om_world_random_scene / om_world_basic_scene  front-end builders  main.rs:37-110
+ *   om_material_*         Material::new_*                           materials.rs:27-38
+ *   om_camera_new         Camera::new                               camera.rs:38-59
+ *   om_upload_world       HittableList::freeze -> FrozenHittableList  hits.rs:87-89, 116-185
+ *   om_render / om_render_device   render_thread::render (all threads of main.rs:200-214)
+ *                                                                   render_thread.rs:145-202
+ *   om_pixel_stats        Pixel/Stats                               render_thread.rs:9-51
+ */
+#ifndef OTTOMARCHER_H
+#define OTTOMARCHER_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OM_ABI_VERSION 1
+
+typedef int32_t om_status;
+#define OM_OK 0
+#define OM_ERR_INVALID (-1)      /* bad argument / null pointer / size */
+#define OM_ERR_DEVICE (-2)       /* HIP runtime error */
+#define OM_ERR_STATE (-3)        /* call order (e.g. render before upload) */
+#define OM_ERR_UNSUPPORTED (-4)  /* feature not representable on the device */
+#define OM_ERR_NOMEM (-5)
+
+/* materials.rs:12-24 — 24 bytes, same field meaning as the Rust struct. */
+enum { OM_LAMBERTIAN = 0, OM_METAL = 1, OM_DIELECTRIC = 2 };
+typedef struct om_material {
+    float albedo[3]; /* Lambertian, Metal */
+    float fuzz;      /* Metal */
+    float ior;       /* Dielectric */
+    int32_t type;    /* OM_LAMBERTIAN / OM_METAL / OM_DIELECTRIC */
+} om_material;
+
+/* camera.rs:10-29 (all derived fields, as Camera::new computes them). */
+typedef struct om_camera {
+    float origin[3], horizontal[3], vertical[3], lower_left_corner[3];
+    float u_of_plane[3], v_of_plane[3], w_of_plane[3];
+    float lens_radius, aspect_ratio, focus_dist, viewport_width, viewport_height;
+} om_camera;
+
+/* Per-pixel accumulator = Stats (render_thread.rs:9-17), 40 bytes.
+ * obj ids are global type-order primitive index + 1 (0 = sky), replacing the
+ * memory address of utils.rs:110; bloom uses them unchanged (utils.rs:94-107). */
+typedef struct om_pixel_stats {
+    uint64_t bloom;     /* BloomFilter.state */
+    float sum[3];       /* Stats.sum */
+    uint32_t n;         /* Stats.n (samples taken) */
+    float avg_depth;    /* Stats.avg_depth */
+    uint32_t bad_avgs;  /* Stats.bad_avgs */
+    uint8_t color[3];   /* Stats.color (gamma-quantised mean) */
+    uint8_t flags;      /* bit0: done (bad_avgs >= 5, adaptive retirement) */
+    uint32_t reserved;
+} om_pixel_stats;
+
+/* One render call = samples [sample_begin, sample_begin+sample_count) of every
+ * (live) pixel, accumulated into the caller's om_pixel_stats in sample order.
+ * spp_total sizes the jitter table (render_thread.rs:164-174); a pixel's sample
+ * index is its Stats.n, exactly as jitters[pixel.stats.n] (render_thread.rs:188). */
+typedef struct om_render_params {
+    uint32_t width, height;     /* image_width / image_height */
+    uint32_t spp_total;         /* samples_per_pixel of the whole frame */
+    uint32_t sample_begin;      /* informative: n of the first sample of this call */
+    uint32_t sample_count;      /* samples per pixel in this call */
+    uint32_t max_depth;         /* max_depth (main.rs:146) */
+    float tmin, tmax;           /* 0.001 / 100.0 (main.rs:205-206) */
+    uint32_t march_steps;       /* max march iterations (hits.rs:292 hard-codes 1024) */
+    uint32_t adaptive;          /* 1 = retire pixels like Stats::add/ThreadPixels (render_thread.rs:31-38,97-101) */
+    uint64_t seed;              /* om-rng v1 seed (replaces thread_rng, utils.rs:25) */
+} om_render_params;
+
+/* Kernel choices (all produce bit-identical om_pixel_stats). */
+enum {
+    OM_KERNEL_AUTO = 0,        /* fastest available for the uploaded world */
+    OM_KERNEL_BRUTE = 1,       /* reference-order brute force, every primitive tested */
+    OM_KERNEL_CULLED = 2,      /* brute force + conservative bounding-sphere pre-test */
+    OM_KERNEL_BVH = 3          /* BVH traversal with the brute-force tie rule */
+};
+
+/* Work counters of the last render call (device atomics, wave-aggregated). */
+typedef struct om_counters {
+    uint64_t samples;           /* samples taken */
+    uint64_t segments;          /* closest-hit queries (ray segments) */
+    uint64_t prim_tests;        /* exact primitive tests executed */
+    uint64_t pre_tests;         /* culling tests executed (bounding spheres / BVH boxes) */
+    uint64_t march_steps;       /* sphere-tracing iterations */
+    uint64_t credited;          /* progress credit as samples_atom (render_thread.rs:196-198) */
+} om_counters;
+
+typedef struct om_world om_world;   /* HittableList (host) */
+typedef struct om_ctx om_ctx;       /* one device + stream + frozen world */
+
+int32_t om_abi_version(void);
+
+/* ---- materials (materials.rs:27-38) ---- */
+om_material om_material_lambertian(float r, float g, float b);
+om_material om_material_metal(float r, float g, float b);
+om_material om_material_metal_fuzz(float r, float g, float b, float fuzz);
+om_material om_material_dielectric(float ior);
+
+/* ---- Mat4x4 helpers (f32, reference op order) so front-ends compose the
+ * m4x4!(TR/RX/RY/RZ/SC) transforms of main.rs with identical bits.
+ * Row-major out[16] = Mat4x4.e[row].e[col]. ---- */
+om_status om_mat4_identity(float out[16]);                                            /* mat4x4.rs:16 */
+om_status om_mat4_translate(const float v[3], float out[16]);                         /* mat4x4.rs:88-93 */
+om_status om_mat4_scale(const float v[3], float out[16]);                             /* mat4x4.rs:94-99 */
+om_status om_mat4_rotate(int32_t axis /*0=x,1=y,2=z*/, float angle, float out[16]);  /* mat4x4.rs:100-123 */
+om_status om_mat4_mul(const float a[16], const float b[16], float out[16]);          /* a ^ b: dot_mat mat4x4.rs:66-72,167-178 */
+om_status om_mat4_fast_homogenous_inverse(const float m[16], float out[16]);        /* mat4x4.rs:59-64 */
+
+/* ---- camera (camera.rs:38-59) ---- */
+om_status om_camera_new(const float lookfrom[3], const float lookat[3], const float vup[3], float vfov_deg,
+                        float aspect_ratio, float aperture, float focus_dist, om_camera* out);
+
+/* ---- world (HittableList) ---- */
+om_status om_world_create(om_world** out);
+void om_world_destroy(om_world* w);
+om_status om_world_clear(om_world* w);
+/* local_to_world: row-major 4x4 (Mat4x4.e[row].e[col]) */
+om_status om_world_add_sphere(om_world* w, const float local_to_world[16], const om_material* m);
+om_status om_world_add_sphere_radius(om_world* w, const float center[3], float radius, const om_material* m);
+om_status om_world_add_cube(om_world* w, const float local_to_world[16], const om_material* m);
+om_status om_world_add_cube_length(om_world* w, const float center[3], float length, const om_material* m);
+om_status om_world_add_triangle(om_world* w, const float origin[3], const float upoint[3], const float vpoint[3], const om_material* m);
+om_status om_world_add_parallelogram(om_world* w, const float origin[3], const float upoint[3], const float vpoint[3], const om_material* m);
+om_status om_world_add_triangle_basis(om_world* w, const float origin[3], const float u[3], const float v[3], float u_length, float v_length, const om_material* m);
+om_status om_world_add_parallelogram_basis(om_world* w, const float origin[3], const float u[3], const float v[3], float u_length, float v_length, const om_material* m);
+om_status om_world_add_plane(om_world* w, const float center[3], const float normal[3], const om_material* m);
+om_status om_world_add_marched_sphere(om_world* w, const float center[3], float radius, const om_material* m);
+om_status om_world_add_marched_box(om_world* w, const float center[3], const float sizes[3], const om_material* m);
+om_status om_world_add_marched_torus(om_world* w, const float local_to_world[16], const float sizes[3], const om_material* m);
+/* counts[8] in type order: spheres, cubes, triangles, infinite_planes, parallelograms,
+ * marched_spheres, marched_boxes, marched_torus (hits.rs:370-371) */
+om_status om_world_counts(const om_world* w, uint32_t counts[8]);
+/* Frozen per-primitive data, for cross-checks (layouts in DESIGN.md §4):
+ * kind 0 sphere / 1 cube -> 32 floats (l2w, w2l); kind 2 triangle / 4 parallelogram -> 29 floats;
+ * kind 7 torus -> 43 floats. */
+om_status om_world_export(const om_world* w, int32_t kind, uint32_t index, float* out, uint32_t out_floats);
+
+/* Front-end scene builders (main.rs:37-110) driven by om-rng v1 from `seed`.
+ * flags bit0: include the marched torus block (main.rs:73-81);
+ * flags bit1: omit the parallelogram/triangle/cube blocks.
+ * grid_half: 11 = random_scene's -11..11 grid; 50 = the 10k-sphere variant. */
+om_status om_world_random_scene(om_world* w, uint64_t seed, uint32_t flags, int32_t grid_half);
+om_status om_world_basic_scene(om_world* w);       /* main.rs:103-110 */
+om_status om_world_marched_scene(om_world* w);     /* SDF scene for config C2 */
+
+/* ---- device context ---- */
+om_status om_create(int32_t device, om_ctx** out);
+void om_destroy(om_ctx* ctx);
+const char* om_last_error(const om_ctx* ctx);      /* ctx may be NULL: last global error */
+/* freeze(): copies the world to device memory (the caller may destroy `w` afterwards).
+ * Arc<dyn Traced/Marched> user types (hits.rs:91-100) cannot cross the C-ABI. */
+om_status om_upload_world(om_ctx* ctx, const om_world* w);
+om_status om_set_kernel(om_ctx* ctx, int32_t kernel);
+/* Host framebuffer path: `stats` is caller-owned W*H, read and written in place
+ * (like PixelsBox, main.rs:192).  Includes the PCIe copies. */
+om_status om_render(om_ctx* ctx, const om_camera* cam, const om_render_params* p, om_pixel_stats* stats,
+                    om_counters* counters /* optional */);
+/* Device framebuffer path: `dev_stats` is device memory (W*H om_pixel_stats) on ctx's
+ * device; `stream` is a hipStream_t (NULL = ctx's own stream).  Asynchronous:
+ * returns after enqueue; the caller synchronises the stream. */
+om_status om_render_device(om_ctx* ctx, const om_camera* cam, const om_render_params* p, om_pixel_stats* dev_stats,
+                           void* stream);
+/* Renders only the pixels listed in `dev_pixels` (device array of row-major pixel
+ * indices) — the tile-shard entry point for multi-GPU frames. */
+om_status om_render_device_pixels(om_ctx* ctx, const om_camera* cam, const om_render_params* p, om_pixel_stats* dev_stats,
+                                  const uint32_t* dev_pixels, uint32_t n_pixels, void* stream);
+/* Work counters of the most recent render on ctx (synchronises ctx's stream). */
+om_status om_get_counters(om_ctx* ctx, om_counters* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OTTOMARCHER_H */

@@ -1,0 +1,174 @@
+// om_bvh.cpp — binned-SAH BVH over spheres, cubes, triangles, parallelograms.
+#include "om_bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+namespace om {
+namespace {
+
+struct Box {
+    double lo[3], hi[3];
+    void empty() { for (int i = 0; i < 3; ++i) { lo[i] = 1e300; hi[i] = -1e300; } }
+    void grow(const Box& b) { for (int i = 0; i < 3; ++i) { lo[i] = std::min(lo[i], b.lo[i]); hi[i] = std::max(hi[i], b.hi[i]); } }
+    void grow_pt(const double* p) { for (int i = 0; i < 3; ++i) { lo[i] = std::min(lo[i], p[i]); hi[i] = std::max(hi[i], p[i]); } }
+    double area() const {
+        const double dx = std::max(0.0, hi[0] - lo[0]), dy = std::max(0.0, hi[1] - lo[1]), dz = std::max(0.0, hi[2] - lo[2]);
+        return 2.0 * (dx * dy + dy * dz + dz * dx);
+    }
+};
+
+struct Item { Box b; double c[3]; uint32_t gi; };
+
+// Inflate a box well beyond f32 rounding of the exact tests.
+Box inflate(Box b) {
+    double mag = 0.0;
+    for (int i = 0; i < 3; ++i) mag = std::max(mag, std::max(std::fabs(b.lo[i]), std::fabs(b.hi[i])));
+    for (int i = 0; i < 3; ++i) {
+        const double ext = b.hi[i] - b.lo[i];
+        const double m = 1e-3 * (1.0 + ext) + 1e-5 * mag;
+        b.lo[i] -= m; b.hi[i] += m;
+    }
+    return b;
+}
+
+Box affine_box(const Mat4& l2w, double half) {
+    Box b;
+    for (int i = 0; i < 3; ++i) {
+        const double a0 = l2w.r[i].e[0], a1 = l2w.r[i].e[1], a2 = l2w.r[i].e[2], c = l2w.r[i].e[3];
+        // sphere (half < 0): exact ellipsoid extent = row norm; cube: 0.5 * L1 row norm
+        const double h = half < 0 ? std::sqrt(a0 * a0 + a1 * a1 + a2 * a2) : half * (std::fabs(a0) + std::fabs(a1) + std::fabs(a2));
+        b.lo[i] = c - h; b.hi[i] = c + h;
+    }
+    return inflate(b);
+}
+
+Box bary_box(const BaryPrim& p, bool para) {
+    Box b; b.empty();
+    double o[3], pu[3], pv[3], puv[3];
+    for (int i = 0; i < 3; ++i) {
+        o[i] = p.origin.e[i];
+        pu[i] = o[i] + (double)p.u.e[i] * p.u_length;
+        pv[i] = o[i] + (double)p.v.e[i] * p.v_length;
+        puv[i] = pu[i] + (double)p.v.e[i] * p.v_length;
+    }
+    b.grow_pt(o); b.grow_pt(pu); b.grow_pt(pv);
+    if (para) b.grow_pt(puv);
+    return inflate(b);
+}
+
+struct Builder {
+    std::vector<Item> items;
+    std::vector<OmBvhNode> nodes;
+    std::vector<uint32_t> order;
+
+    uint32_t emit(const Box& b) {
+        OmBvhNode n;
+        for (int i = 0; i < 3; ++i) {
+            n.lo[i] = std::nextafter((float)b.lo[i], -INFINITY);
+            n.hi[i] = std::nextafter((float)b.hi[i], INFINITY);
+        }
+        n.left = 0; n.right = 0;
+        nodes.push_back(n);
+        return (uint32_t)(nodes.size() - 1);
+    }
+
+    // builds items[begin,end) ; returns node index
+    uint32_t build(uint32_t begin, uint32_t end) {
+        Box bb; bb.empty(); Box cb; cb.empty();
+        for (uint32_t i = begin; i < end; ++i) { bb.grow(items[i].b); cb.grow_pt(items[i].c); }
+        const uint32_t node = emit(bb);
+        const uint32_t count = end - begin;
+        auto make_leaf = [&]() {
+            nodes[node].left = -(int32_t)(order.size() + 1);
+            nodes[node].right = (int32_t)count;
+            for (uint32_t i = begin; i < end; ++i) order.push_back(items[i].gi);
+            return node;
+        };
+        if (count <= 2) return make_leaf();
+        // binned SAH over the centroid box
+        const int NB = 16;
+        double best_cost = 1e300; int best_axis = -1; int best_bin = -1;
+        for (int ax = 0; ax < 3; ++ax) {
+            const double lo = cb.lo[ax], hi = cb.hi[ax];
+            if (!(hi - lo > 1e-12)) continue;
+            Box bins[NB]; uint32_t cnt[NB] = {0};
+            for (int k = 0; k < NB; ++k) bins[k].empty();
+            for (uint32_t i = begin; i < end; ++i) {
+                int k = (int)((items[i].c[ax] - lo) / (hi - lo) * NB);
+                k = std::min(NB - 1, std::max(0, k));
+                bins[k].grow(items[i].b); cnt[k]++;
+            }
+            Box lacc; lacc.empty(); uint32_t lc = 0;
+            double la[NB]; uint32_t lcs[NB];
+            for (int k = 0; k < NB - 1; ++k) { lacc.grow(bins[k]); lc += cnt[k]; la[k] = lacc.area(); lcs[k] = lc; }
+            Box racc; racc.empty(); uint32_t rc = 0;
+            for (int k = NB - 1; k > 0; --k) {
+                racc.grow(bins[k]); rc += cnt[k];
+                const uint32_t lcount = lcs[k - 1];
+                if (lcount == 0 || rc == 0) continue;
+                const double cost = la[k - 1] * lcount + racc.area() * rc;
+                if (cost < best_cost) { best_cost = cost; best_axis = ax; best_bin = k; }
+            }
+        }
+        const double leaf_cost = bb.area() * count;
+        const double trav = 1.0 * bb.area();  // traversal cost relative to one primitive test
+        if (best_axis < 0) {
+            if (count <= 8) return make_leaf();
+            // degenerate centroids: median split on the longest box axis
+            int ax = 0;
+            for (int k = 1; k < 3; ++k) if (bb.hi[k] - bb.lo[k] > bb.hi[ax] - bb.lo[ax]) ax = k;
+            std::nth_element(items.begin() + begin, items.begin() + begin + count / 2, items.begin() + end,
+                             [ax](const Item& x, const Item& y) { return x.c[ax] < y.c[ax]; });
+            const uint32_t mid = begin + count / 2;
+            const uint32_t l = build(begin, mid);
+            const uint32_t r = build(mid, end);
+            nodes[node].left = (int32_t)l; nodes[node].right = (int32_t)r;
+            return node;
+        }
+        if (count <= 8 && leaf_cost <= best_cost + trav) return make_leaf();
+        const int ax = best_axis;
+        const double lo = cb.lo[ax], hi = cb.hi[ax];
+        auto mid_it = std::partition(items.begin() + begin, items.begin() + end, [&](const Item& it) {
+            int k = (int)((it.c[ax] - lo) / (hi - lo) * NB);
+            k = std::min(NB - 1, std::max(0, k));
+            return k < best_bin;
+        });
+        uint32_t mid = (uint32_t)(mid_it - items.begin());
+        if (mid == begin || mid == end) mid = begin + count / 2;
+        const uint32_t l = build(begin, mid);
+        const uint32_t r = build(mid, end);
+        nodes[node].left = (int32_t)l; nodes[node].right = (int32_t)r;
+        return node;
+    }
+};
+
+}  // namespace
+
+void build_bvh(const om_world& w, FrozenWorld& fw) {
+    Builder b;
+    std::vector<uint32_t> always;
+    const double kHuge = 100.0;  // a bound larger than this is tested outside the BVH
+    auto add = [&](const Box& box, uint32_t gi) {
+        double ext = 0.0;
+        for (int i = 0; i < 3; ++i) ext = std::max(ext, box.hi[i] - box.lo[i]);
+        if (ext > 2.0 * kHuge) { always.push_back(gi); return; }
+        Item it; it.b = box; it.gi = gi;
+        for (int i = 0; i < 3; ++i) it.c[i] = 0.5 * (box.lo[i] + box.hi[i]);
+        b.items.push_back(it);
+    };
+    for (size_t i = 0; i < w.spheres.size(); ++i) add(affine_box(w.spheres[i].l2w, -1.0), fw.offsets[K_SPHERE] + (uint32_t)i);
+    for (size_t i = 0; i < w.cubes.size(); ++i) add(affine_box(w.cubes[i].l2w, 0.5), fw.offsets[K_CUBE] + (uint32_t)i);
+    for (size_t i = 0; i < w.triangles.size(); ++i) add(bary_box(w.triangles[i], false), fw.offsets[K_TRI] + (uint32_t)i);
+    for (size_t i = 0; i < w.planes.size(); ++i) always.push_back(fw.offsets[K_PLANE] + (uint32_t)i);
+    for (size_t i = 0; i < w.parallelograms.size(); ++i) add(bary_box(w.parallelograms[i], true), fw.offsets[K_PARA] + (uint32_t)i);
+    std::sort(always.begin(), always.end());
+    fw.always = always;
+    if (!b.items.empty()) b.build(0, (uint32_t)b.items.size());
+    fw.bvh = b.nodes;
+    fw.bvh_prims = b.order;
+}
+
+}  // namespace om

@@ -1,0 +1,123 @@
+// om_layout.h — frozen-world layout in HBM (host builder <-> HIP kernels).
+//
+// The reference keeps one typed Vec per primitive type (hits.rs:34-69, order
+// hits.rs:370-371).  The frozen device world keeps that order but splits every
+// primitive into a hot "test" record (what a miss needs: 64 B, read by every
+// lane of a wave at the same address -> scalar loads) and a cold "hit" record
+// (what the winner needs to build its HitRecord).  Global primitive index gi
+// follows the type order; obj_id = gi + 1 (0 = sky).
+#pragma once
+#include <stdint.h>
+
+#define OM_ALIGN16 __attribute__((aligned(16)))
+
+// Affine primitive (Sphere traced.rs:13-19, Cube traced.rs:229-235).
+// w2l rows 0..2 (row-major 3x4); dz[i] = w2l[i][3] * 0.0f — the w-term of
+// Mat4x4::dot_v3 (mat4x4.rs:54-57) kept so signed zeros match bit for bit.
+struct OM_ALIGN16 OmAffineTest {
+    float w2l[12];
+    float dz[3];
+    float pad;
+};
+struct OM_ALIGN16 OmAffineHit {
+    float l2w[12];
+    float lz[3];  // l2w[i][3] * 0.0f
+    float pad;
+};
+// Conservative world-space bounding sphere of an affine primitive: center, and
+// the inflated radius squared.  Used only to skip exact tests
+// that would return None.
+struct OM_ALIGN16 OmBound {
+    float c[3];
+    float r;     // inflated radius
+};
+
+// Barycentric<BT> (traced.rs:118-131) — only what hit_aux reads.
+struct OM_ALIGN16 OmBary {
+    float origin[3];
+    float u_length;
+    float uxv[3];
+    float v_length;
+    float base_inv[9];
+    float vx, vy;     // v_in_base.x, v_in_base.z (calc_barycentric traced.rs:156-167)
+    float pad;
+};
+// InfinitePlane (traced.rs:77-82)
+struct OM_ALIGN16 OmPlane {
+    float center[3];
+    float pad0;
+    float normal[3];
+    float pad1;
+};
+// MarchedSphere (marched.rs:50-54), MarchedBox (marched.rs:79-83)
+struct OM_ALIGN16 OmMSphere {
+    float center[3];
+    float radius;
+};
+struct OM_ALIGN16 OmMBox {
+    float center[3];
+    float pad0;
+    float sizes[3];
+    float pad1;
+};
+// MarchedTorus (marched.rs:105-113)
+struct OM_ALIGN16 OmMTorus {
+    float l2w_tr[16];
+    float w2l_tr[16];
+    float l2w_s[4];
+    float w2l_s[4];
+    float sizes[3];
+    float min_scale;  // l2w_s.xyz().min_val() (marched.rs:148-150), precomputed
+};
+// Material (materials.rs:18-24), padded to 32 B.
+struct OM_ALIGN16 OmMaterial {
+    float albedo[3];
+    float fuzz;
+    float ior;
+    int32_t type;
+    float pad[2];
+};
+
+// BVH node (binary, 32 B).  Internal: left/right children; leaf: [first, first+count)
+// into the prim index list.  Boxes are conservative (inflated).
+struct OM_ALIGN16 OmBvhNode {
+    float lo[3];
+    int32_t left;     // >=0 internal: index of left child; <0 leaf: -(first+1)
+    float hi[3];
+    int32_t right;    // internal: index of right child; leaf: count
+};
+
+// Device view of a frozen world (passed by value as a kernel argument).
+struct OmSceneDev {
+    const OmAffineTest* sph_test; const OmAffineHit* sph_hit; const OmBound* sph_bound;
+    const OmAffineTest* cube_test; const OmAffineHit* cube_hit; const OmBound* cube_bound;
+    const OmBary* tri; const OmPlane* plane; const OmBary* para;
+    const OmMSphere* msph; const OmMBox* mbox; const OmMTorus* mtor;
+    const OmMaterial* mats;       // by global index gi
+    const uint64_t* bloom;        // by obj_id (gi + 1); bloom[0] = 0
+    const OmBvhNode* bvh;         // over bounded traced prims (spheres, cubes, tris, paras)
+    const uint32_t* bvh_prims;    // leaf -> global index gi
+    uint32_t n_sph, n_cube, n_tri, n_plane, n_para, n_msph, n_mbox, n_mtor;
+    uint32_t n_bvh_nodes;
+    uint32_t n_always;            // number of unbounded/huge prims tested outside the BVH
+    const uint32_t* always;       // their global indices (ascending)
+    // type offsets of the global index space
+    uint32_t off_cube, off_tri, off_plane, off_para, off_msph, off_mbox, off_mtor, n_total;
+};
+
+struct OmCamDev {
+    float origin[3], horizontal[3], vertical[3], llc_minus_origin[3];
+    float u[3], v[3];
+    float lens_radius;
+};
+
+struct OmParamsDev {
+    uint32_t width, height, spp_total, sample_count, max_depth, march_steps, adaptive;
+    float tmin, tmax, wf_m1, hf_m1;   // (W-1), (H-1) as f32
+    uint64_t skey;                     // mix64(seed + K) (om-rng v1)
+    uint32_t n_pixels;                 // pixels this launch covers
+    uint32_t tiles_x;                  // 8x8 tiles per row (full-frame mapping)
+};
+
+// Counter slots (om_counters order)
+enum { OMC_SAMPLES = 0, OMC_SEGMENTS, OMC_PRIM_TESTS, OMC_PRE_TESTS, OMC_MARCH, OMC_CREDITED, OMC_N };

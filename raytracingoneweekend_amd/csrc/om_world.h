@@ -1,0 +1,55 @@
+// om_world.h — host HittableList and its frozen, device-ready image.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../../include/ottomarcher.h"
+#include "om_hostmath.h"
+#include "om_layout.h"
+
+namespace om {
+
+struct AffinePrim { Mat4 l2w, w2l; om_material mat; };              // Sphere / Cube (traced.rs:13-19, 229-235)
+struct BaryPrim {                                                     // Barycentric<BT> (traced.rs:118-131)
+    Vec3 origin, u; float u_length; Vec3 v; float v_length; Vec3 uxv, uxvxu; Mat3 base_inv; Vec3 v_in_base; om_material mat;
+};
+struct PlanePrim { Vec3 center, normal; om_material mat; };          // InfinitePlane (traced.rs:77-82)
+struct MSpherePrim { Vec3 center; float radius; om_material mat; };  // marched.rs:50-54
+struct MBoxPrim { Vec3 center, sizes; om_material mat; };            // marched.rs:79-83
+struct MTorusPrim { Mat4 l2w_tr, w2l_tr; Vec4 l2w_s, w2l_s; Vec3 sizes; om_material mat; };  // marched.rs:105-113
+
+enum PrimKind { K_SPHERE = 0, K_CUBE = 1, K_TRI = 2, K_PLANE = 3, K_PARA = 4, K_MSPHERE = 5, K_MBOX = 6, K_MTORUS = 7 };
+
+// Frozen image of a world: arrays laid out exactly as they are copied to HBM.
+struct FrozenWorld {
+    std::vector<OmAffineTest> sph_test, cube_test;
+    std::vector<OmAffineHit> sph_hit, cube_hit;
+    std::vector<OmBound> sph_bound, cube_bound;
+    std::vector<OmBary> tri, para;
+    std::vector<OmPlane> plane;
+    std::vector<OmMSphere> msph;
+    std::vector<OmMBox> mbox;
+    std::vector<OmMTorus> mtor;
+    std::vector<OmMaterial> mats;      // by global index
+    std::vector<uint64_t> bloom;       // by obj id
+    std::vector<OmBvhNode> bvh;
+    std::vector<uint32_t> bvh_prims;   // global indices
+    std::vector<uint32_t> always;      // global indices tested outside the BVH
+    uint32_t counts[8];
+    uint32_t offsets[9];               // global index offset per kind, offsets[8] = total
+};
+
+uint64_t bloom_hash(uint64_t id);      // utils.rs:94-107
+
+}  // namespace om
+
+struct om_world {
+    std::vector<om::AffinePrim> spheres, cubes;
+    std::vector<om::BaryPrim> triangles, parallelograms;
+    std::vector<om::PlanePrim> planes;
+    std::vector<om::MSpherePrim> msph;
+    std::vector<om::MBoxPrim> mbox;
+    std::vector<om::MTorusPrim> mtor;
+    void freeze(om::FrozenWorld& fw) const;
+};

@@ -1,0 +1,118 @@
+"""GPU parity: the HIP hot path (through the C-ABI) vs the CPU oracle on the same
+scene, camera, params and om-rng seed.  Bar: bit-identical om_pixel_stats
+(sum, n, avg_depth, bad_avgs, color, flags, bloom) for every pixel, every kernel."""
+import numpy as np
+import pytest
+
+from scenes_common import compare_stats, kitchen_sink
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = ["brute", "culled", "bvh"]
+
+
+def _render_both(om, O, world, oworld, cam, ocam, W, H, spp, kernel, seed=3, max_depth=50, adaptive=False,
+                 sample_count=None, march_steps=1024):
+    frozen = world.freeze(cam, kernel=kernel)
+    pix = om.PixelsBox.new(W * H)
+    om.render(cam, frozen, max_depth, 0.001, 100.0, spp, W, H, pix, seed=seed, adaptive=adaptive,
+              sample_count=sample_count, march_steps=march_steps)
+    p = O.params(W, H, spp, sample_count=sample_count, max_depth=max_depth, adaptive=adaptive, seed=seed,
+                 march_steps=march_steps)
+    exp, _ = O.render(oworld, ocam, p)
+    return pix.pixels, exp, frozen
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_traced_scene_bit_exact(om, oracle, kernel):
+    W, H, SPP = 64, 40, 6
+    got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED), oracle.random_scene(0x5EED),
+                               om.default_camera(W / H), oracle.default_camera(W / H), W, H, SPP, kernel)
+    nb, msg = compare_stats(got, exp, f"S-traced/{kernel}")
+    assert nb == 0, msg
+    assert (got["n"] == SPP).all()
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_full_scene_with_torus_bit_exact(om, oracle, kernel):
+    W, H, SPP = 40, 28, 3
+    got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED, with_torus=True),
+                               oracle.random_scene(0x5EED, with_torus=True),
+                               om.default_camera(W / H), oracle.default_camera(W / H), W, H, SPP, kernel)
+    nb, msg = compare_stats(got, exp, f"S-full/{kernel}")
+    assert nb == 0, msg
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_kitchen_sink_every_primitive_bit_exact(om, oracle, kernel):
+    W, H, SPP = 48, 32, 4
+    w, ow, cam, ocam = kitchen_sink(om, oracle)
+    got, exp, _ = _render_both(om, oracle, w, ow, cam, ocam, W, H, SPP, kernel, seed=11)
+    nb, msg = compare_stats(got, exp, f"kitchen/{kernel}")
+    assert nb == 0, msg
+
+
+def test_marched_scene_bit_exact(om, oracle):
+    W, H, SPP = 32, 20, 2
+    got, exp, _ = _render_both(om, oracle, om.marched_scene(), oracle.marched_scene(), om.default_camera(W / H),
+                               oracle.default_camera(W / H), W, H, SPP, "auto", march_steps=256)
+    nb, msg = compare_stats(got, exp, "S-marched")
+    assert nb == 0, msg
+
+
+def test_adaptive_retirement_bit_exact(om, oracle):
+    W, H, SPP = 32, 24, 24
+    got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED), oracle.random_scene(0x5EED),
+                               om.default_camera(W / H), oracle.default_camera(W / H), W, H, SPP, "auto",
+                               adaptive=True)
+    nb, msg = compare_stats(got, exp, "adaptive")
+    assert nb == 0, msg
+    assert got["n"].min() < SPP  # some pixels (sky) retired early, like the reference
+
+
+def test_progressive_calls_equal_single_call(om):
+    W, H = 40, 24
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam)
+    a = om.PixelsBox.new(W * H)
+    om.render(cam, fz, 50, 0.001, 100.0, 8, W, H, a, seed=5)
+    b = om.PixelsBox.new(W * H)
+    for _ in range(4):
+        om.render(cam, fz, 50, 0.001, 100.0, 8, W, H, b, seed=5, sample_count=2)
+    nb, msg = compare_stats(b.pixels, a.pixels, "progressive")
+    assert nb == 0, msg
+
+
+def test_shallow_depth_and_exhaustion(om, oracle):
+    # max_depth 1 and 0: every hit path ends with -Color::ZERO (render_thread.rs:142)
+    W, H = 24, 16
+    for depth in (0, 1, 2):
+        got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED), oracle.random_scene(0x5EED),
+                                   om.default_camera(W / H), oracle.default_camera(W / H), W, H, 2, "auto",
+                                   max_depth=depth)
+        nb, msg = compare_stats(got, exp, f"depth{depth}")
+        assert nb == 0, msg
+
+
+def test_ten_k_scene_bvh_bit_exact(om, oracle):
+    W, H, SPP = 32, 18, 2
+    got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED, grid_half=50, extras=False),
+                               oracle.random_scene(0x5EED, grid_half=50, extras=False),
+                               om.default_camera(W / H), oracle.default_camera(W / H), W, H, SPP, "bvh")
+    nb, msg = compare_stats(got, exp, "S-10k")
+    assert nb == 0, msg
+
+
+def test_counters_consistent(om):
+    W, H, SPP = 32, 16, 4
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    for k in KERNELS:
+        fz = world.freeze(cam, kernel=k)
+        pix = om.PixelsBox.new(W * H)
+        c = om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=2)
+        assert c["samples"] == W * H * SPP
+        assert c["segments"] >= c["samples"]
+        if k == "brute":
+            assert c["prim_tests"] == c["segments"] * 485
