@@ -1,0 +1,206 @@
+"""bench.py — MI355X benchmark of the ray_color hot path (BASELINE.json metric).
+
+Workload (config C1, BASELINE.json configs[1]): the S-traced random_scene (main.rs:37-100
+minus the torus block, om-rng scene seed 0x5EED), camera of main.rs:136-142, 1920x1080,
+max_depth 50, tmin 0.001, tmax 100, fixed spp (adaptive off).  One STEP = one progressive
+pass of SPP_PER_STEP samples over every pixel this rank owns, accumulated into the
+per-pixel Stats in HBM (render_thread.rs:176-199, batched).  32 steps at N=1 = the full
+512-spp frame.
+
+N>1 (torch.distributed.run, one rank per GPU): 8x8 pixel tiles are dealt round-robin to
+ranks (main.rs:172-189's chunk round-robin); every rank renders its tiles at
+SPP_PER_STEP*N samples per step (fixed per-GPU work: weak scaling) and one RCCL gather
+of the finished f32 framebuffer to rank 0 closes the timed region.
+
+Output: ONE JSON line on rank 0 (see DESIGN.md §7 for every field).
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import raytracingoneweekend_amd as om  # noqa: E402
+from raytracingoneweekend_amd import _lib as L  # noqa: E402
+from raytracingoneweekend_amd import shard  # noqa: E402
+
+W, H, MAX_DEPTH, TMIN, TMAX, SEED, SCENE_SEED = 1920, 1080, 50, 0.001, 100.0, 1, 0x5EED
+SPP_PER_STEP = 16
+PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md; FMA = 2 flop)
+PEAK_HBM_GBS = 8000.0
+
+# Algorithmic FP32 work per counted unit, counted from om_device.h /
+# om_render.hip in the reference's op order (no FMA: every add/mul/div/sqrt/min/max/cmp = 1).
+FLOP_EXACT_TEST = 56      # Sphere::hit miss path: 2 affine xforms (36) + a, half_b, c, disc, cmp (20)
+FLOP_BOX_TEST = 25        # slab test of one BVH child box
+FLOP_SEGMENT = 110        # finalize (point + normal) + scatter + throughput + loop bookkeeping
+FLOP_SAMPLE = 95          # jitter/uv + lens disc + get_ray + Stats::add
+FLOP_MARCH_STEP = 60      # one sphere-tracing iteration over the marched objects (S-traced: none)
+# HBM bytes per unit: Stats read + write once per pixel per launch (40 B each way)
+BYTES_PER_PIXEL_LAUNCH = 80
+
+
+def cpu_baseline(budget_s=12.0):
+    """Oracle (CPU restatement, `port`) on the host: the reference's thread scheme
+    (num_cpus-1 workers, 2730-px round-robin chunks, main.rs:170-189) on the same C1 frame."""
+    from oracle import oracle as O  # checker / baseline only
+    cores = max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 2)) - 1)
+    ow = O.random_scene(SCENE_SEED)
+    cam = O.default_camera(W / H)
+    done, t_total, passes = 0, 0.0, 0
+    stats = np.zeros(W * H, dtype=O.PIXEL_STATS_DTYPE)
+    spp_total = 64
+    while passes == 0 or (t_total < budget_s and passes < spp_total):
+        p = O.params(W, H, spp_total, sample_count=1, max_depth=MAX_DEPTH, seed=SEED)
+        t0 = time.perf_counter()
+        _, ctr = O.render(ow, cam, p, stats=stats, nthreads=cores)
+        t_total += time.perf_counter() - t0
+        done += ctr["samples"]
+        passes += 1
+    return {"value": done / t_total / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
+            "sample": f"C1 frame {W}x{H}, {passes} spp (full passes), depth {MAX_DEPTH}, S-traced, "
+                      f"{cores} threads, {t_total:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
+    torch.cuda.set_device(local_rank)
+    if world_size > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    # ---- setup (not timed): scene build + freeze/upload, camera, tile lists
+    # a dedicated (non-NULL) stream: the kernel, its HIP events and the collectives all run on it
+    stream = torch.cuda.Stream()
+    torch.cuda.set_stream(stream)
+    sptr = C.c_void_p(stream.cuda_stream)
+    assert sptr.value, "need a non-default stream handle"
+    world = om.random_scene(SCENE_SEED)
+    cam = om.default_camera(W / H)
+    frozen = world.freeze(cam, device=local_rank, kernel=args.kernel)
+    ctx = frozen.ctx
+    spp_step = SPP_PER_STEP * world_size                     # fixed per-GPU samples per step
+    spp_total = spp_step * args.steps
+    pix = shard.tile_pixels(W, H, rank, world_size)
+    n_px = int(pix.size)
+    dev_pix = torch.from_numpy(pix.view(np.int32)).cuda()
+    stats = torch.zeros(n_px * 40, dtype=torch.uint8, device="cuda")
+
+    def step(p):
+        L.check(L.lib.om_render_device_pixels(ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(stats.data_ptr()),
+                                              C.c_void_p(dev_pix.data_ptr()), n_px, sptr), ctx)
+
+    p = om.make_params(MAX_DEPTH, TMIN, TMAX, spp_total, W, H, sample_count=spp_step, seed=SEED)
+    for _ in range(args.warmup):
+        step(p)
+    torch.cuda.synchronize()
+    stats.zero_()                                            # timed frame starts from empty Stats
+    L.check(L.lib.om_reset_counters(ctx, sptr), ctx)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    gathered, send = None, None
+    if world_size > 1:                                       # gather buffers (equal-size shards), allocated untimed
+        n_max = shard.shard_capacity(W, H, world_size) * 40
+        send = torch.zeros(n_max, dtype=torch.uint8, device="cuda")
+        gathered = [torch.empty_like(send) for _ in range(world_size)] if rank == 0 else None
+    torch.cuda.synchronize()
+
+    # ---- timed region
+    if world_size > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step(p)
+        ev[k][1].record(stream)
+    if world_size > 1:                                       # RCCL gather of the f32 framebuffer to rank 0
+        send[: stats.numel()] = stats
+        dist.gather(send, gathered, dst=0)
+    torch.cuda.synchronize()
+    if world_size > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    # ---- end timed region
+
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if world_size > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    launch_ms = [a.elapsed_time(b) for a, b in ev]
+    ctr = L.om_counters()
+    L.check(L.lib.om_get_counters(ctx, C.byref(ctr)), ctx)
+    host = stats.cpu().numpy().view(L.PIXEL_STATS_DTYPE)
+    assert int(host["n"].min()) == spp_total and int(host["n"].max()) == spp_total, "every pixel must take every sample"
+
+    total_samples = W * H * spp_total                          # all ranks together
+    value = total_samples / elapsed / 1e6
+
+    # roofline of the dominant kernel (render_kernel), per launch, from the live counters
+    avg_launch_s = float(np.mean(launch_ms)) / 1e3
+    flops = (FLOP_EXACT_TEST * ctr.prim_tests + FLOP_BOX_TEST * ctr.pre_tests + FLOP_SEGMENT * ctr.segments
+             + FLOP_SAMPLE * ctr.samples + FLOP_MARCH_STEP * ctr.march_steps) / args.steps
+    achieved_tflops = flops / avg_launch_s / 1e12
+    hbm_gbs = BYTES_PER_PIXEL_LAUNCH * n_px / avg_launch_s / 1e9
+
+    if rank == 0:
+        if gathered is not None:                             # assemble + verify the gathered frame (untimed)
+            frame = shard.assemble(W, H, [g.cpu().numpy() for g in gathered])
+            assert int(frame["n"].min()) == spp_total, "gathered frame incomplete"
+        cpu = None
+        if world_size == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.cpu_budget)
+        out = {
+            "metric": "Msamples/s (W×H×spp/s) + achieved HBM GB/s, 1080p@512spp traced scene",
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic: S-traced random_scene (om-rng seed 0x5EED), render seed 1",
+            "config": {"workload": f"C1 S-traced {W}x{H}, {spp_total} spp timed ({spp_step} spp/step), depth {MAX_DEPTH}",
+                       "width": W, "height": H, "spp_per_step": spp_step, "max_depth": MAX_DEPTH,
+                       "parallelism": f"tile{world_size}", "kernel": args.kernel},
+            "hbm_gbs": round(hbm_gbs, 2),
+            "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": None,
+                         "kernel": "render_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                         "flop_per_launch": flops},
+            "work": {"segments_per_sample": round(ctr.segments / max(1, ctr.samples), 4),
+                     "prim_tests_per_segment": round(ctr.prim_tests / max(1, ctr.segments), 3),
+                     "box_tests_per_segment": round(ctr.pre_tests / max(1, ctr.segments), 3),
+                     "gsegments_per_s": round(ctr.segments * world_size / elapsed / 1e9, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    if world_size > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

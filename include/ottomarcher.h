@@ -188,8 +188,11 @@ om_status om_render_device(om_ctx* ctx, const om_camera* cam, const om_render_pa
  * indices) — the tile-shard entry point for multi-GPU frames. */
 om_status om_render_device_pixels(om_ctx* ctx, const om_camera* cam, const om_render_params* p, om_pixel_stats* dev_stats,
                                   const uint32_t* dev_pixels, uint32_t n_pixels, void* stream);
-/* Work counters of the most recent render on ctx (synchronises ctx's stream). */
+/* Work counters, accumulated over every om_render_device* launch since the last
+ * om_reset_counters (om_render resets them itself).  om_get_counters synchronises
+ * ctx's stream and the stream of the last launch. */
 om_status om_get_counters(om_ctx* ctx, om_counters* out);
+om_status om_reset_counters(om_ctx* ctx, void* stream);
 
 #ifdef __cplusplus
 }

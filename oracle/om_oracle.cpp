@@ -959,4 +959,15 @@ void oro_render(void* wp, const OroCamera* c, const RenderParams* p, void* stats
     }
 }
 
+// Pixel-subset render (tile shards): stats[k] belongs to pixels[k].  Single thread.
+void oro_render_pixels(void* wp, const OroCamera* c, const RenderParams* p, void* stats_v, const uint32_t* pixels, uint32_t n) {
+    World* w = (World*)wp; w->assign_ids(); w->march_steps = p->march_steps;
+    Camera cam = cam_from(c);
+    PixelStats* stats = (PixelStats*)stats_v;
+    std::vector<float> jt = jitter_table(p->seed, p->spp_total);
+    uint64_t skey = seed_key(p->seed);
+    Counters ctr{0, 0, 0};
+    for (uint32_t k = 0; k < n; ++k) render_pixel(*w, cam, *p, jt.data(), skey, pixels[k], stats[k], ctr);
+}
+
 }  // extern "C"

@@ -73,6 +73,8 @@ def _load():
         "oro_marched_sdf": (C.c_float, [vp, C.c_int, C.c_uint32, fp]),
         "oro_marched_normal": (None, [vp, C.c_int, C.c_uint32, fp, fp]),
         "oro_render": (None, [vp, C.POINTER(OroCamera), C.POINTER(OroParams), vp, C.c_int32, C.POINTER(C.c_uint64)]),
+        "oro_render_pixels": (None, [vp, C.POINTER(OroCamera), C.POINTER(OroParams), vp, C.POINTER(C.c_uint32),
+                                     C.c_uint32]),
     }
     for n, (r, a) in sig.items():
         f = getattr(lib, n)
@@ -211,6 +213,15 @@ def render(world, cam, p, stats=None, nthreads=0):
     ctr = (C.c_uint64 * 3)()
     lib.oro_render(world.h, C.byref(cam), C.byref(p), stats.ctypes.data_as(C.c_void_p), int(nthreads), ctr)
     return stats, {"samples": ctr[0], "segments": ctr[1], "credited": ctr[2]}
+
+
+def render_pixels(world, cam, p, pixels):
+    """Render only `pixels` (uint32 row-major indices); returns compact stats[len(pixels)]."""
+    pixels = np.ascontiguousarray(pixels, dtype=np.uint32)
+    stats = np.zeros(pixels.size, dtype=PIXEL_STATS_DTYPE)
+    lib.oro_render_pixels(world.h, C.byref(cam), C.byref(p), stats.ctypes.data_as(C.c_void_p),
+                          pixels.ctypes.data_as(C.POINTER(C.c_uint32)), pixels.size)
+    return stats
 
 
 def rng_draws(state, n):

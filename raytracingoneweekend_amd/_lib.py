@@ -57,7 +57,7 @@ EXPORTS = [
     "om_world_add_marched_box", "om_world_add_marched_torus", "om_world_counts", "om_world_export",
     "om_world_random_scene", "om_world_basic_scene", "om_world_marched_scene", "om_create", "om_destroy",
     "om_last_error", "om_upload_world", "om_set_kernel", "om_render", "om_render_device",
-    "om_render_device_pixels", "om_get_counters",
+    "om_render_device_pixels", "om_get_counters", "om_reset_counters",
 ]
 
 
@@ -117,6 +117,7 @@ def _load():
         "om_render_device": (st, [vp, C.POINTER(om_camera), C.POINTER(om_render_params), vp, vp]),
         "om_render_device_pixels": (st, [vp, C.POINTER(om_camera), C.POINTER(om_render_params), vp, vp, C.c_uint32, vp]),
         "om_get_counters": (st, [vp, C.POINTER(om_counters)]),
+        "om_reset_counters": (st, [vp, vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -405,6 +405,7 @@ struct om_ctx {
     int kernel = OM_KERNEL_AUTO;
     DevBuf counters, jitter, stats, pixels;
     uint64_t jitter_seed = 0; uint32_t jitter_spp = 0;
+    hipStream_t last_stream = nullptr;
     ~om_ctx() {
         for (auto& b : scene_bufs) b.release();
         counters.release(); jitter.release(); stats.release(); pixels.release();
@@ -485,9 +486,12 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
                  const uint32_t* dev_pixels, uint32_t n_pixels, hipStream_t stream) {
     om_status s = prepare_jitter(c, p->seed, p->spp_total);
     if (s) return s;
-    s = ensure(c, c->counters, OMC_N * sizeof(unsigned long long));
-    if (s) return s;
-    OM_HIP(c, hipMemsetAsync(c->counters.p, 0, OMC_N * sizeof(unsigned long long), stream));
+    if (!c->counters.p) {
+        s = ensure(c, c->counters, OMC_N * sizeof(unsigned long long));
+        if (s) return s;
+        OM_HIP(c, hipMemsetAsync(c->counters.p, 0, OMC_N * sizeof(unsigned long long), stream));
+    }
+    c->last_stream = stream;
     OmCamDev C;
     for (int i = 0; i < 3; ++i) {
         C.origin[i] = cam->origin[i]; C.horizontal[i] = cam->horizontal[i]; C.vertical[i] = cam->vertical[i];
@@ -633,6 +637,7 @@ om_status om_render(om_ctx* c, const om_camera* cam, const om_render_params* p, 
     const size_t bytes = (size_t)p->width * p->height * sizeof(om_pixel_stats);
     if ((s = ensure(c, c->stats, bytes)) != OM_OK) return s;
     OM_HIP(c, hipMemcpyAsync(c->stats.p, stats, bytes, hipMemcpyHostToDevice, c->stream));
+    if ((s = om_reset_counters(c, c->stream)) != OM_OK) return s;
     if ((s = launch(c, cam, p, (om_pixel_stats*)c->stats.p, nullptr, 0, c->stream)) != OM_OK) return s;
     OM_HIP(c, hipMemcpyAsync(stats, c->stats.p, bytes, hipMemcpyDeviceToHost, c->stream));
     OM_HIP(c, hipStreamSynchronize(c->stream));
@@ -647,9 +652,19 @@ om_status om_get_counters(om_ctx* c, om_counters* out) {
     OM_HIP(c, hipSetDevice(c->device));
     unsigned long long h[OMC_N];
     OM_HIP(c, hipStreamSynchronize(c->stream));
+    if (c->last_stream && c->last_stream != c->stream) OM_HIP(c, hipStreamSynchronize(c->last_stream));
     OM_HIP(c, hipMemcpy(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
     out->samples = h[OMC_SAMPLES]; out->segments = h[OMC_SEGMENTS]; out->prim_tests = h[OMC_PRIM_TESTS];
     out->pre_tests = h[OMC_PRE_TESTS]; out->march_steps = h[OMC_MARCH]; out->credited = h[OMC_CREDITED];
+    return OM_OK;
+}
+
+om_status om_reset_counters(om_ctx* c, void* stream) {
+    if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
+    OM_HIP(c, hipSetDevice(c->device));
+    om_status s = ensure(c, c->counters, OMC_N * sizeof(unsigned long long));
+    if (s) return s;
+    OM_HIP(c, hipMemsetAsync(c->counters.p, 0, OMC_N * sizeof(unsigned long long), stream ? (hipStream_t)stream : c->stream));
     return OM_OK;
 }
 
