@@ -76,6 +76,7 @@ def main():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
+    ap.add_argument("--pipeline", default="wavefront", choices=list(L.PIPELINES))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -97,7 +98,7 @@ def main():
     assert sptr.value, "need a non-default stream handle"
     world = om.random_scene(SCENE_SEED)
     cam = om.default_camera(W / H)
-    frozen = world.freeze(cam, device=local_rank, kernel=args.kernel)
+    frozen = world.freeze(cam, device=local_rank, kernel=args.kernel, pipeline=args.pipeline)
     ctx = frozen.ctx
     spp_step = SPP_PER_STEP * world_size                     # fixed per-GPU samples per step
     spp_total = spp_step * args.steps
@@ -115,7 +116,11 @@ def main():
         step(p)
     torch.cuda.synchronize()
     stats.zero_()                                            # timed frame starts from empty Stats
-    L.check(L.lib.om_reset_counters(ctx, sptr), ctx)
+    L.check(L.lib.om_set_counting(ctx, 0), ctx)              # production build: counters compiled out
+    for _ in range(args.warmup):                             # warm the non-counting kernel too
+        step(p)
+    torch.cuda.synchronize()
+    stats.zero_()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     gathered, send = None, None
     if world_size > 1:                                       # gather buffers (equal-size shards), allocated untimed
@@ -147,10 +152,20 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     launch_ms = [a.elapsed_time(b) for a, b in ev]
+    host = stats.cpu().numpy().view(L.PIXEL_STATS_DTYPE).copy()
+    assert int(host["n"].min()) == spp_total and int(host["n"].max()) == spp_total, "every pixel must take every sample"
+
+    # work counting (untimed): the same K launches again with the counting build; the
+    # frame it produces must equal the timed one bit for bit (counters change nothing)
+    stats.zero_()
+    L.check(L.lib.om_reset_counters(ctx, sptr), ctx)
+    L.check(L.lib.om_set_counting(ctx, 1), ctx)
+    for _ in range(args.steps):
+        step(p)
+    torch.cuda.synchronize()
     ctr = L.om_counters()
     L.check(L.lib.om_get_counters(ctx, C.byref(ctr)), ctx)
-    host = stats.cpu().numpy().view(L.PIXEL_STATS_DTYPE)
-    assert int(host["n"].min()) == spp_total and int(host["n"].max()) == spp_total, "every pixel must take every sample"
+    assert np.array_equal(stats.cpu().numpy(), host.view(np.uint8)), "counting build changed the result"
 
     total_samples = W * H * spp_total                          # all ranks together
     value = total_samples / elapsed / 1e6
@@ -184,7 +199,7 @@ def main():
             "data": "synthetic: S-traced random_scene (om-rng seed 0x5EED), render seed 1",
             "config": {"workload": f"C1 S-traced {W}x{H}, {spp_total} spp timed ({spp_step} spp/step), depth {MAX_DEPTH}",
                        "width": W, "height": H, "spp_per_step": spp_step, "max_depth": MAX_DEPTH,
-                       "parallelism": f"tile{world_size}", "kernel": args.kernel},
+                       "parallelism": f"tile{world_size}", "kernel": args.kernel, "pipeline": args.pipeline},
             "hbm_gbs": round(hbm_gbs, 2),
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": None,

@@ -96,7 +96,8 @@ enum {
     OM_KERNEL_AUTO = 0,        /* fastest available for the uploaded world */
     OM_KERNEL_BRUTE = 1,       /* reference-order brute force, every primitive tested */
     OM_KERNEL_CULLED = 2,      /* brute force + conservative bounding-sphere pre-test */
-    OM_KERNEL_BVH = 3          /* BVH traversal with the brute-force tie rule */
+    OM_KERNEL_BVH = 3,         /* stack-based BVH traversal (global memory) with the brute-force tie rule */
+    OM_KERNEL_SBVH = 4         /* stackless skip-pointer BVH, staged in LDS when it fits (default) */
 };
 
 /* Work counters of the last render call (device atomics, wave-aggregated). */
@@ -193,6 +194,15 @@ om_status om_render_device_pixels(om_ctx* ctx, const om_camera* cam, const om_re
  * ctx's stream and the stream of the last launch. */
 om_status om_get_counters(om_ctx* ctx, om_counters* out);
 om_status om_reset_counters(om_ctx* ctx, void* stream);
+/* Work counting on (default) / off.  Off selects kernel builds with the counters
+ * compiled out (fewer registers); results are bit-identical either way. */
+om_status om_set_counting(om_ctx* ctx, int32_t enable);
+/* Execution pipeline (both bit-identical):
+ *   OM_PIPELINE_WAVEFRONT  (default) raygen -> {intersect -> shade+compact} per bounce -> accumulate,
+ *                          SoA ray queues in HBM
+ *   OM_PIPELINE_MEGAKERNEL one persistent-path kernel per call */
+enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1 };
+om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
 
 #ifdef __cplusplus
 }

@@ -14,8 +14,11 @@ LIB_PATH = os.path.join(_HERE, "libottomarcher.so")
 OM_OK = 0
 OM_ERR_INVALID, OM_ERR_DEVICE, OM_ERR_STATE, OM_ERR_UNSUPPORTED, OM_ERR_NOMEM = -1, -2, -3, -4, -5
 OM_LAMBERTIAN, OM_METAL, OM_DIELECTRIC = 0, 1, 2
-OM_KERNEL_AUTO, OM_KERNEL_BRUTE, OM_KERNEL_CULLED, OM_KERNEL_BVH = 0, 1, 2, 3
-KERNELS = {"auto": OM_KERNEL_AUTO, "brute": OM_KERNEL_BRUTE, "culled": OM_KERNEL_CULLED, "bvh": OM_KERNEL_BVH}
+OM_KERNEL_AUTO, OM_KERNEL_BRUTE, OM_KERNEL_CULLED, OM_KERNEL_BVH, OM_KERNEL_SBVH = 0, 1, 2, 3, 4
+KERNELS = {"auto": OM_KERNEL_AUTO, "brute": OM_KERNEL_BRUTE, "culled": OM_KERNEL_CULLED, "bvh": OM_KERNEL_BVH,
+           "sbvh": OM_KERNEL_SBVH}
+OM_PIPELINE_MEGAKERNEL, OM_PIPELINE_WAVEFRONT = 0, 1
+PIPELINES = {"megakernel": OM_PIPELINE_MEGAKERNEL, "wavefront": OM_PIPELINE_WAVEFRONT}
 
 F3 = C.c_float * 3
 F16 = C.c_float * 16
@@ -57,7 +60,7 @@ EXPORTS = [
     "om_world_add_marched_box", "om_world_add_marched_torus", "om_world_counts", "om_world_export",
     "om_world_random_scene", "om_world_basic_scene", "om_world_marched_scene", "om_create", "om_destroy",
     "om_last_error", "om_upload_world", "om_set_kernel", "om_render", "om_render_device",
-    "om_render_device_pixels", "om_get_counters", "om_reset_counters",
+    "om_render_device_pixels", "om_get_counters", "om_reset_counters", "om_set_counting", "om_set_pipeline",
 ]
 
 
@@ -65,7 +68,19 @@ class OmError(RuntimeError):
     pass
 
 
+def _share_hip_runtime_with_torch():
+    """PyTorch-ROCm ships its own libamdhip64 (same soname).  Loading torch first makes
+    libottomarcher.so bind to that one runtime, so torch tensors/streams and this
+    library share a single HIP runtime in the process (two runtimes cannot both own
+    the device).  torch is optional for the C-ABI itself."""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
+
+
 def _load():
+    _share_hip_runtime_with_torch()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `make -C raytracingoneweekend_amd/csrc` "
@@ -118,6 +133,8 @@ def _load():
         "om_render_device_pixels": (st, [vp, C.POINTER(om_camera), C.POINTER(om_render_params), vp, vp, C.c_uint32, vp]),
         "om_get_counters": (st, [vp, C.POINTER(om_counters)]),
         "om_reset_counters": (st, [vp, vp]),
+        "om_set_counting": (st, [vp, C.c_int32]),
+        "om_set_pipeline": (st, [vp, C.c_int32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -285,20 +285,25 @@ class HittableList:
         check(lib.om_world_export(self._w, int(kind), int(index), fptr(out), n))
         return np.array(list(out), dtype=np.float32)
 
-    def freeze(self, cam=None, device=0, kernel="auto"):
+    def freeze(self, cam=None, device=0, kernel="auto", pipeline="wavefront"):
         """hits.rs:87-89: snapshot to device memory (the camera is unused: the camera hash is out of scope)."""
-        return FrozenHittableList(self, device=device, kernel=kernel)
+        return FrozenHittableList(self, device=device, kernel=kernel, pipeline=pipeline)
 
 
 class FrozenHittableList:
     """hits.rs:63-69 — a world resident in HBM on one device (om_ctx)."""
 
-    def __init__(self, world, device=0, kernel="auto"):
+    def __init__(self, world, device=0, kernel="auto", pipeline="wavefront"):
         self._ctx = C.c_void_p()
         check(lib.om_create(int(device), C.byref(self._ctx)))
         check(lib.om_upload_world(self._ctx, world.handle), self._ctx)
         self.set_kernel(kernel)
+        self.set_pipeline(pipeline)
         self.device = device
+
+    def set_pipeline(self, pipeline):
+        check(lib.om_set_pipeline(self._ctx, L.PIPELINES[pipeline] if isinstance(pipeline, str) else int(pipeline)),
+              self._ctx)
 
     def set_kernel(self, kernel):
         check(lib.om_set_kernel(self._ctx, L.KERNELS[kernel] if isinstance(kernel, str) else int(kernel)), self._ctx)

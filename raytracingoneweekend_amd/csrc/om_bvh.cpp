@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <vector>
 
 namespace om {
@@ -169,6 +170,65 @@ void build_bvh(const om_world& w, FrozenWorld& fw) {
     if (!b.items.empty()) b.build(0, (uint32_t)b.items.size());
     fw.bvh = b.nodes;
     fw.bvh_prims = b.order;
+    build_skip_bvh(w, fw);
+}
+
+// Stackless layout: the SAH tree over the affine primitives (spheres,
+// cubes) re-emitted in depth-first order with a skip ("miss") link per node, and the
+// primitives' test records copied in leaf order so a leaf owns a contiguous run.
+// Everything else (planes, triangles, parallelograms, huge bounds) goes to always2.
+void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
+    Builder b;
+    std::vector<uint32_t> always;
+    const double kHuge = 100.0;
+    auto add = [&](const Box& box, uint32_t gi) {
+        double ext = 0.0;
+        for (int i = 0; i < 3; ++i) ext = std::max(ext, box.hi[i] - box.lo[i]);
+        if (ext > 2.0 * kHuge) { always.push_back(gi); return; }
+        Item it; it.b = box; it.gi = gi;
+        for (int i = 0; i < 3; ++i) it.c[i] = 0.5 * (box.lo[i] + box.hi[i]);
+        b.items.push_back(it);
+    };
+    for (size_t i = 0; i < w.spheres.size(); ++i) add(affine_box(w.spheres[i].l2w, -1.0), fw.offsets[K_SPHERE] + (uint32_t)i);
+    for (size_t i = 0; i < w.cubes.size(); ++i) add(affine_box(w.cubes[i].l2w, 0.5), fw.offsets[K_CUBE] + (uint32_t)i);
+    for (size_t i = 0; i < w.triangles.size(); ++i) always.push_back(fw.offsets[K_TRI] + (uint32_t)i);
+    for (size_t i = 0; i < w.planes.size(); ++i) always.push_back(fw.offsets[K_PLANE] + (uint32_t)i);
+    for (size_t i = 0; i < w.parallelograms.size(); ++i) always.push_back(fw.offsets[K_PARA] + (uint32_t)i);
+    std::sort(always.begin(), always.end());
+    fw.always2 = always;
+    fw.snodes.clear();
+    fw.srecs.clear();
+    if (b.items.empty()) return;
+    const uint32_t root = b.build(0, (uint32_t)b.items.size());
+    // depth-first re-emission with skip links
+    struct Emit {
+        const Builder& b; const FrozenWorld& fw; std::vector<OmSkipNode>& out; std::vector<OmAffineTest>& recs;
+        void rec(uint32_t n) {
+            const OmBvhNode& src = b.nodes[n];
+            const uint32_t idx = (uint32_t)out.size();
+            OmSkipNode o;
+            for (int i = 0; i < 3; ++i) { o.lo[i] = src.lo[i]; o.hi[i] = src.hi[i]; }
+            o.skip = 0; o.leaf = 0xFFFFFFFFu;
+            out.push_back(o);
+            if (src.left < 0) {
+                const uint32_t first = (uint32_t)(-src.left - 1), cnt = (uint32_t)src.right;
+                out[idx].leaf = ((uint32_t)recs.size() << 8) | cnt;
+                for (uint32_t k = 0; k < cnt; ++k) {
+                    const uint32_t gi = b.order[first + k];
+                    const bool cube = gi >= fw.offsets[K_CUBE];
+                    OmAffineTest t = cube ? fw.cube_test[gi - fw.offsets[K_CUBE]] : fw.sph_test[gi];
+                    const uint32_t tag = gi | (cube ? 0x80000000u : 0u);
+                    std::memcpy(&t.pad, &tag, 4);
+                    recs.push_back(t);
+                }
+            } else {
+                rec((uint32_t)src.left);
+                rec((uint32_t)src.right);
+            }
+            out[idx].skip = (uint32_t)out.size();
+        }
+    } e{b, fw, fw.snodes, fw.srecs};
+    e.rec(root);
 }
 
 }  // namespace om

@@ -10,4 +10,5 @@
 
 namespace om {
 void build_bvh(const om_world& w, FrozenWorld& fw);
+void build_skip_bvh(const om_world& w, FrozenWorld& fw);
 }

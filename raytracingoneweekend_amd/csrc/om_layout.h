@@ -87,6 +87,16 @@ struct OM_ALIGN16 OmBvhNode {
     int32_t right;    // internal: index of right child; leaf: count
 };
 
+// Stackless BVH node (32 B), depth-first order: on a box hit go to idx+1 (internal)
+// or test the leaf's records then go to `skip`; on a miss go to `skip`.
+// leaf = (first_record << 8) | count, or 0xFFFFFFFF for an internal node.
+struct OM_ALIGN16 OmSkipNode {
+    float lo[3];
+    uint32_t skip;
+    float hi[3];
+    uint32_t leaf;
+};
+
 // Device view of a frozen world (passed by value as a kernel argument).
 struct OmSceneDev {
     const OmAffineTest* sph_test; const OmAffineHit* sph_hit; const OmBound* sph_bound;
@@ -103,6 +113,10 @@ struct OmSceneDev {
     const uint32_t* always;       // their global indices (ascending)
     // type offsets of the global index space
     uint32_t off_cube, off_tri, off_plane, off_para, off_msph, off_mbox, off_mtor, n_total;
+    // stackless BVH over the affine primitives (records carry gi | cube<<31 in `pad`)
+    const OmSkipNode* snodes; const OmAffineTest* srecs; const uint32_t* always2;
+    uint32_t n_snodes, n_srecs, n_always2;
+    uint32_t lds_bytes;           // dynamic LDS the staged kernel needs (0 = scene too big: global path)
 };
 
 struct OmCamDev {

@@ -23,6 +23,7 @@
 #include "../../include/ottomarcher.h"
 #include "om_device.h"
 #include "om_layout.h"
+#include "om_wavefront.h"
 #include "om_world.h"
 
 using namespace omd;
@@ -37,198 +38,15 @@ constexpr int kBlock = 256;
 // ---------------------------------------------------------------------------
 // closest hit over the traced primitives
 // ---------------------------------------------------------------------------
-enum { MODE_BRUTE = 1, MODE_CULLED = 2, MODE_BVH = 3 };
+enum { MODE_BRUTE = 1, MODE_CULLED = 2, MODE_BVH = 3, MODE_SBVH_LDS = 4, MODE_SBVH_GLOBAL = 5 };
+constexpr int kBlockLds = 512;
+constexpr uint32_t kLdsBudget = 96u * 1024u;   // staged scene per workgroup (160 KiB per CU)
 
-struct Work { uint32_t prim, pre, march; };
+}  // namespace
 
-// Exact test of global primitive gi with the brute-force acceptance (root <= tmax).
-__device__ __forceinline__ bool test_prim(const OmSceneDev& S, uint32_t gi, F3 o, F3 d, float tmin, float tmax, float& t) {
-    if (gi < S.off_cube) return sphere_root(S.sph_test[gi], o, d, tmin, tmax, t);
-    if (gi < S.off_tri) { int ax; return cube_root(S.cube_test[gi - S.off_cube], o, d, tmin, tmax, t, ax); }
-    float ndd;
-    if (gi < S.off_plane) return bary_root<true>(S.tri[gi - S.off_tri], o, d, tmin, tmax, t, ndd);
-    if (gi < S.off_para) return plane_root(S.plane[gi - S.off_plane], o, d, tmin, tmax, t, ndd);
-    return bary_root<false>(S.para[gi - S.off_para], o, d, tmin, tmax, t, ndd);
-}
+#include "om_trace.h"
 
-// Reference order brute force: FrozenHittableList::hit traced section (hits.rs:272-285).
-// CULL: skip spheres whose conservative bounding sphere proves the exact test
-// would return None — the accepted sequence is unchanged.
-template <bool CULL>
-__device__ __forceinline__ int traced_brute(const OmSceneDev& S, F3 o, F3 d, float tmin, float& closest, Work& w) {
-    int best = -1;
-    float t;
-    for (uint32_t i = 0; i < S.n_sph; ++i) {
-        if (CULL) {
-            const OmBound B = S.sph_bound[i];
-            const float ocx = o.x - B.c[0], ocy = o.y - B.c[1], ocz = o.z - B.c[2];
-            const float b = ocx * d.x + ocy * d.y + ocz * d.z;
-            const float px = ocx - b * d.x, py = ocy - b * d.y, pz = ocz - b * d.z;
-            const float q = px * px + py * py + pz * pz;
-            w.pre++;
-            // every comparison is false for NaN -> the exact test decides
-            if (q > B.r * B.r || -b + B.r < tmin || -b - B.r > closest) continue;
-        }
-        w.prim++;
-        if (sphere_root(S.sph_test[i], o, d, tmin, closest, t)) { closest = t; best = (int)i; }
-    }
-    for (uint32_t i = 0; i < S.n_cube; ++i) {
-        int ax; w.prim++;
-        if (cube_root(S.cube_test[i], o, d, tmin, closest, t, ax)) { closest = t; best = (int)(S.off_cube + i); }
-    }
-    float ndd;
-    for (uint32_t i = 0; i < S.n_tri; ++i) {
-        w.prim++;
-        if (bary_root<true>(S.tri[i], o, d, tmin, closest, t, ndd)) { closest = t; best = (int)(S.off_tri + i); }
-    }
-    for (uint32_t i = 0; i < S.n_plane; ++i) {
-        w.prim++;
-        if (plane_root(S.plane[i], o, d, tmin, closest, t, ndd)) { closest = t; best = (int)(S.off_plane + i); }
-    }
-    for (uint32_t i = 0; i < S.n_para; ++i) {
-        w.prim++;
-        if (bary_root<false>(S.para[i], o, d, tmin, closest, t, ndd)) { closest = t; best = (int)(S.off_para + i); }
-    }
-    return best;
-}
-
-// BVH traversal with the brute-force tie rule: the reference keeps the smallest
-// accepted root and, on equal roots, the later object in type order.
-__device__ __forceinline__ void offer(const OmSceneDev& S, uint32_t gi, F3 o, F3 d, float tmin, float& closest, int& best, Work& w) {
-    float t;
-    w.prim++;
-    if (test_prim(S, gi, o, d, tmin, closest, t)) {
-        if (t < closest || (int)gi > best) { closest = t; best = (int)gi; }
-    }
-}
-
-__device__ __forceinline__ int traced_bvh(const OmSceneDev& S, F3 o, F3 d, float tmin, float& closest, Work& w) {
-    // Non-finite rays take the reference loop (NaN roots are accepted there).
-    if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return traced_brute<false>(S, o, d, tmin, closest, w);
-    int best = -1;
-    for (uint32_t k = 0; k < S.n_always; ++k) offer(S, S.always[k], o, d, tmin, closest, best, w);
-    if (S.n_bvh_nodes == 0) return best;
-    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
-    const float t_lo = tmin * 0.5f - 1e-3f;
-    uint32_t stack[64];
-    int sp = 0;
-    uint32_t node = 0;
-    for (;;) {
-        const OmBvhNode N = S.bvh[node];
-        if (N.left < 0) {
-            const uint32_t first = (uint32_t)(-N.left - 1), cnt = (uint32_t)N.right;
-            for (uint32_t k = 0; k < cnt; ++k) offer(S, S.bvh_prims[first + k], o, d, tmin, closest, best, w);
-        } else {
-            const OmBvhNode L = S.bvh[N.left], R = S.bvh[N.right];
-            w.pre += 2;
-            // Slab tests on inflated boxes, (lo - o) * (1/d): a zero direction component
-            // gives +-inf (correct containment) or NaN (dropped by fminf/fmaxf = unconstrained).
-            const float t_hi = closest * 1.0001f + 1e-3f;
-            float x0 = (L.lo[0] - o.x) * ix, x1 = (L.hi[0] - o.x) * ix;
-            float y0 = (L.lo[1] - o.y) * iy, y1 = (L.hi[1] - o.y) * iy;
-            float z0 = (L.lo[2] - o.z) * iz, z1 = (L.hi[2] - o.z) * iz;
-            const float ln = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-            const float lf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
-            x0 = (R.lo[0] - o.x) * ix; x1 = (R.hi[0] - o.x) * ix;
-            y0 = (R.lo[1] - o.y) * iy; y1 = (R.hi[1] - o.y) * iy;
-            z0 = (R.lo[2] - o.z) * iz; z1 = (R.hi[2] - o.z) * iz;
-            const float rn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-            const float rf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
-            const bool hl = ln <= lf, hr = rn <= rf;
-            if (hl && hr) {
-                const bool left_first = ln <= rn;
-                stack[sp++] = left_first ? (uint32_t)N.right : (uint32_t)N.left;
-                node = left_first ? (uint32_t)N.left : (uint32_t)N.right;
-                continue;
-            }
-            if (hl) { node = (uint32_t)N.left; continue; }
-            if (hr) { node = (uint32_t)N.right; continue; }
-        }
-        if (sp == 0) break;
-        node = stack[--sp];
-    }
-    return best;
-}
-
-// unstuck (hits.rs:336-365) + sphere-tracing loop (hits.rs:287-333).
-// Returns the marched winner's global index or -1; `t` receives the hit t.
-__device__ __forceinline__ int march(const OmSceneDev& S, F3 o, F3 d, float tmin, float tmax, float closest,
-                                     uint32_t steps, float& t_hit, Work& w) {
-    const float HIT = 0.001f;
-    // nearest marched object at r.at(tmin), strict '<' (first minimum wins)
-    F3 p = at(o, d, tmin);
-    float dist = INFINITY; int kind = -1; uint32_t idx = 0;
-    for (uint32_t i = 0; i < S.n_msph; ++i) { const float v = fabsf(msphere_sdf(S.msph[i], p)); if (v < dist) { dist = v; kind = 0; idx = i; } }
-    for (uint32_t i = 0; i < S.n_mbox; ++i) { const float v = fabsf(mbox_sdf(S.mbox[i], p)); if (v < dist) { dist = v; kind = 1; idx = i; } }
-    for (uint32_t i = 0; i < S.n_mtor; ++i) { const float v = fabsf(mtorus_sdf(S.mtor[i], p)); if (v < dist) { dist = v; kind = 2; idx = i; } }
-    if (kind < 0) return -1;                                                   // hits.rs:359
-    float t = tmin;
-    float aux = dist;
-    uint32_t guard = 0;
-    while (aux < HIT && guard++ < (1u << 22)) {                                // hits.rs:360-363 (+ safety cap)
-        t += HIT / 2.0f;
-        const F3 q = at(o, d, t);
-        aux = kind == 0 ? fabsf(msphere_sdf(S.msph[idx], q)) : kind == 1 ? fabsf(mbox_sdf(S.mbox[idx], q)) : fabsf(mtorus_sdf(S.mtor[idx], q));
-    }
-    uint32_t iters = steps;
-    while (t < tmax && t < closest && iters > 0) {                            // hits.rs:294
-        iters -= 1;
-        w.march++;
-        p = at(o, d, t);
-        float best = INFINITY; int bk = -1; uint32_t bi = 0;
-        for (uint32_t i = 0; i < S.n_msph; ++i) { const float v = fabsf(msphere_sdf(S.msph[i], p)); if (v < best) { best = v; bk = 0; bi = i; } }
-        for (uint32_t i = 0; i < S.n_mbox; ++i) { const float v = fabsf(mbox_sdf(S.mbox[i], p)); if (v < best) { best = v; bk = 1; bi = i; } }
-        for (uint32_t i = 0; i < S.n_mtor; ++i) { const float v = fabsf(mtorus_sdf(S.mtor[i], p)); if (v < best) { best = v; bk = 2; bi = i; } }
-        if (bk < 0) return -1;                                                 // hits.rs:323
-        if (best < HIT) {                                                      // hits.rs:325-327
-            t_hit = t;
-            return (int)(bk == 0 ? S.off_msph + bi : bk == 1 ? S.off_mbox + bi : S.off_mtor + bi);
-        }
-        t += best;                                                             // hits.rs:330
-    }
-    return -1;
-}
-
-// Build the HitRecord of the winner (point, normal) — the winner's own exact
-// test re-run with tmax = its root reproduces the same root bit for bit.
-__device__ __forceinline__ void finalize(const OmSceneDev& S, int gi, F3 o, F3 d, float tmin, float t, F3& point, F3& normal) {
-    const uint32_t g = (uint32_t)gi;
-    if (g < S.off_tri) {                                                       // Sphere / Cube
-        const bool cube = g >= S.off_cube;
-        const OmAffineTest& T = cube ? S.cube_test[g - S.off_cube] : S.sph_test[g];
-        const OmAffineHit& H = cube ? S.cube_hit[g - S.off_cube] : S.sph_hit[g];
-        const F3 lo = xform_p(T.w2l, o), ld = xform_v(T.w2l, T.dz, d);
-        const F3 lp = at(lo, ld, t);
-        point = xform_p(H.l2w, lp);
-        if (!cube) {
-            normal = unit(xform_v(H.l2w, H.lz, lp));                           // traced.rs:59
-        } else {
-            float r; int ax = 0;
-            cube_root(T, o, d, tmin, t, r, ax);
-            // traced.rs:293-296: axis * copysign(1, p[idx]); normal NOT normalised
-            const float comp = ax == 0 ? lp.x : (ax == 1 ? lp.y : lp.z);
-            const float s = copysignf(1.0f, comp);
-            const F3 ln = f3((ax == 0 ? 1.0f : 0.0f) * s, (ax == 1 ? 1.0f : 0.0f) * s, (ax == 2 ? 1.0f : 0.0f) * s);
-            normal = xform_v(H.l2w, H.lz, ln);
-        }
-        return;
-    }
-    if (g < S.off_msph) {                                                      // plane / barycentric
-        F3 n, c;
-        if (g < S.off_plane) { n = ld3(S.tri[g - S.off_tri].uxv); c = ld3(S.tri[g - S.off_tri].origin); }
-        else if (g < S.off_para) { n = ld3(S.plane[g - S.off_plane].normal); c = ld3(S.plane[g - S.off_plane].center); }
-        else { n = ld3(S.para[g - S.off_para].uxv); c = ld3(S.para[g - S.off_para].origin); }
-        float r, ndd;
-        plane_isect(n, c, o, d, r, ndd);
-        point = at(o, d, t);
-        normal = scl(n, copysignf(1.0f, -ndd));                                // traced.rs:101-103
-        return;
-    }
-    point = at(o, d, t);                                                       // marched (hits.rs:326)
-    if (g < S.off_mbox) normal = msphere_normal(S.msph[g - S.off_msph], point);
-    else if (g < S.off_mtor) normal = mbox_normal(S.mbox[g - S.off_mbox], point);
-    else normal = mtorus_normal(S.mtor[g - S.off_mtor], point);
-}
+namespace {
 
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
@@ -236,13 +54,26 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void render_kernel(OmSceneDev S, OmCamDev C, OmParamsDev P,
-                                                        const float2* __restrict__ jitter,
-                                                        om_pixel_stats* __restrict__ stats,
-                                                        const uint32_t* __restrict__ pixel_list,
-                                                        unsigned long long* __restrict__ counters) {
-    const uint32_t tid = blockIdx.x * kBlock + threadIdx.x;
+extern __shared__ __attribute__((aligned(16))) uint4 om_lds[];
+
+template <int MODE, int BLOCK, bool COUNT>
+__global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(OmSceneDev S, OmCamDev C, OmParamsDev P,
+                                                       const float2* __restrict__ jitter,
+                                                       om_pixel_stats* __restrict__ stats,
+                                                       const uint32_t* __restrict__ pixel_list,
+                                                       unsigned long long* __restrict__ counters) {
+    if (MODE == MODE_SBVH_LDS) {
+        // stage the stackless BVH + its records once per workgroup (uint4 chunks)
+        const uint32_t nn = S.n_snodes * 2u, nr = S.n_srecs * 4u;
+        const uint4* sn = (const uint4*)S.snodes;
+        const uint4* sr = (const uint4*)S.srecs;
+        for (uint32_t i = threadIdx.x; i < nn; i += BLOCK) om_lds[i] = sn[i];
+        for (uint32_t i = threadIdx.x; i < nr; i += BLOCK) om_lds[nn + i] = sr[i];
+        __syncthreads();
+    }
+    const OmSkipNode* lds_nodes = (const OmSkipNode*)om_lds;
+    const OmAffineTest* lds_recs = (const OmAffineTest*)(om_lds + S.n_snodes * 2u);
+    const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t pixel, slot;
     bool valid;
     if (pixel_list) {
@@ -277,7 +108,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(OmSceneDev S, OmCamDev C
     Rng g; g.s = 0;
     uint32_t seg = 0, first_id = 0;
     float depthf = 0.0f;
-    Work w = {0, 0, 0};
+    WorkT<COUNT> w;
     uint32_t n_samples = 0, n_segments = 0, credited = 0;
 
     for (;;) {
@@ -315,10 +146,12 @@ __global__ __launch_bounds__(kBlock) void render_kernel(OmSceneDev S, OmCamDev C
         if (!live) continue;
 
         // ---- one segment: handle_hit(world.hit(ray)) render_thread.rs:105-126
-        n_segments++;
+        if (COUNT) n_segments++;
         float closest = P.tmax;
         int best;
-        if (MODE == MODE_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
+        if (MODE == MODE_SBVH_LDS) best = traced_sbvh(S, lds_nodes, lds_recs, o, d, P.tmin, closest, w);
+        else if (MODE == MODE_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
+        else if (MODE == MODE_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
         else best = traced_brute<MODE == MODE_CULLED>(S, o, d, P.tmin, closest, w);
         if (has_marched) {
             float tm;
@@ -354,8 +187,10 @@ __global__ __launch_bounds__(kBlock) void render_kernel(OmSceneDev S, OmCamDev C
         seg++;
         if (finished) {
             const bool done = stats_add(st, result, rdepth, S.bloom[rid]);
-            n_samples++;
-            credited += ((done && P.adaptive) ? (P.spp_total - st.n) : 0u) + 1u; // :196-198
+            if (COUNT) {
+                n_samples++;
+                credited += ((done && P.adaptive) ? (P.spp_total - st.n) : 0u) + 1u; // :196-198
+            }
             live = false;
         }
     }
@@ -368,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void render_kernel(OmSceneDev S, OmCamDev C
         out.color[2] = (uint8_t)((st.rgbf >> 16) & 0xFFu); out.flags = (uint8_t)(st.rgbf >> 24); out.reserved = 0u;
         stats[slot] = out;
     }
-    if (counters) {
+    if (COUNT) {
         const uint32_t c0 = wave_sum(n_samples), c1 = wave_sum(n_segments), c2 = wave_sum(w.prim), c3 = wave_sum(w.pre),
                        c4 = wave_sum(w.march), c5 = wave_sum(credited);
         if ((threadIdx.x & 63u) == 0u) {
@@ -406,9 +241,15 @@ struct om_ctx {
     DevBuf counters, jitter, stats, pixels;
     uint64_t jitter_seed = 0; uint32_t jitter_spp = 0;
     hipStream_t last_stream = nullptr;
+    bool count_work = true;
+    int pipeline = OM_PIPELINE_WAVEFRONT;
+    omw::Buffers wf;
+    DevBuf frame_list;                  // tile-ordered pixel list of the full frame (wavefront path)
+    uint32_t frame_w = 0, frame_h = 0;
     ~om_ctx() {
         for (auto& b : scene_bufs) b.release();
-        counters.release(); jitter.release(); stats.release(); pixels.release();
+        counters.release(); jitter.release(); stats.release(); pixels.release(); frame_list.release();
+        wf.release();
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -482,6 +323,16 @@ om_status validate(om_ctx* c, const om_camera* cam, const om_render_params* p) {
     return OM_OK;
 }
 
+template <int MODE, int BLOCK>
+void go(bool count, uint64_t threads, uint32_t lds, hipStream_t stream, const OmSceneDev& S, const OmCamDev& C,
+        const OmParamsDev& P, const float2* jt, om_pixel_stats* st, const uint32_t* px, unsigned long long* ctr) {
+    const uint32_t blocks = (uint32_t)((threads + BLOCK - 1) / BLOCK);
+    if (count)
+        hipLaunchKernelGGL((render_kernel<MODE, BLOCK, true>), dim3(blocks), dim3(BLOCK), lds, stream, S, C, P, jt, st, px, ctr);
+    else
+        hipLaunchKernelGGL((render_kernel<MODE, BLOCK, false>), dim3(blocks), dim3(BLOCK), lds, stream, S, C, P, jt, st, px, ctr);
+}
+
 om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_pixel_stats* dev_stats,
                  const uint32_t* dev_pixels, uint32_t n_pixels, hipStream_t stream) {
     om_status s = prepare_jitter(c, p->seed, p->spp_total);
@@ -520,17 +371,57 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         threads = tiles * 64u;
     }
     if (threads == 0) return OM_OK;
-    const uint32_t blocks = (uint32_t)((threads + kBlock - 1) / kBlock);
     int mode = c->kernel;
-    if (mode == OM_KERNEL_AUTO) mode = OM_KERNEL_BVH;
+    if (mode == OM_KERNEL_AUTO) mode = OM_KERNEL_SBVH;
+    if (c->pipeline == OM_PIPELINE_WAVEFRONT) {
+        omw::Launch L;
+        L.S = c->scene; L.C = C; L.P = P;
+        L.jitter = (const float2*)c->jitter.p;
+        L.stats = dev_stats;
+        L.counters = (unsigned long long*)c->counters.p;
+        L.count = c->count_work;
+        L.trace_mode = mode == OM_KERNEL_BRUTE ? MODE_BRUTE : mode == OM_KERNEL_CULLED ? MODE_CULLED
+                     : mode == OM_KERNEL_BVH ? MODE_BVH : MODE_SBVH_LDS;
+        if (dev_pixels) {
+            L.pixels = dev_pixels; L.n_pixels = n_pixels; L.stats_by_pixel = false;
+        } else {
+            if (c->frame_w != p->width || c->frame_h != p->height || !c->frame_list.p) {
+                // 8x8 tiles in row-major tile order, lanes row-major inside a tile
+                std::vector<uint32_t> lst;
+                lst.reserve((size_t)p->width * p->height);
+                const uint32_t tx = (p->width + 7u) / 8u, ty = (p->height + 7u) / 8u;
+                for (uint32_t t = 0; t < tx * ty; ++t)
+                    for (uint32_t l = 0; l < 64u; ++l) {
+                        const uint32_t px = (t % tx) * 8u + (l & 7u), py = (t / tx) * 8u + (l >> 3);
+                        if (px < p->width && py < p->height) lst.push_back(py * p->width + px);
+                    }
+                if ((s = ensure(c, c->frame_list, lst.size() * 4)) != OM_OK) return s;
+                OM_HIP(c, hipMemcpyAsync(c->frame_list.p, lst.data(), lst.size() * 4, hipMemcpyHostToDevice, stream));
+                OM_HIP(c, hipStreamSynchronize(stream));
+                c->frame_w = p->width; c->frame_h = p->height;
+            }
+            L.pixels = (const uint32_t*)c->frame_list.p; L.n_pixels = p->width * p->height; L.stats_by_pixel = true;
+        }
+        std::string err;
+        const hipError_t e = omw::render(c->wf, L, stream, err);
+        if (e != hipSuccess) return set_err(c, OM_ERR_DEVICE, err + ": " + hipGetErrorString(e));
+        return OM_OK;
+    }
     const float2* jt = (const float2*)c->jitter.p;
     unsigned long long* ctr = (unsigned long long*)c->counters.p;
-    if (mode == OM_KERNEL_BRUTE)
-        hipLaunchKernelGGL(render_kernel<MODE_BRUTE>, dim3(blocks), dim3(kBlock), 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
-    else if (mode == OM_KERNEL_CULLED)
-        hipLaunchKernelGGL(render_kernel<MODE_CULLED>, dim3(blocks), dim3(kBlock), 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
-    else
-        hipLaunchKernelGGL(render_kernel<MODE_BVH>, dim3(blocks), dim3(kBlock), 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
+    const bool count = c->count_work;
+    if (mode == OM_KERNEL_SBVH) {
+        if (c->scene.lds_bytes)
+            go<MODE_SBVH_LDS, kBlockLds>(count, threads, c->scene.lds_bytes, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
+        else
+            go<MODE_SBVH_GLOBAL, kBlockLds>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
+    } else if (mode == OM_KERNEL_BRUTE) {
+        go<MODE_BRUTE, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
+    } else if (mode == OM_KERNEL_CULLED) {
+        go<MODE_CULLED, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
+    } else {
+        go<MODE_BVH, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
+    }
     OM_HIP(c, hipGetLastError());
     return OM_OK;
 }
@@ -590,6 +481,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     UP(tri, tri); UP(plane, plane); UP(para, para);
     UP(msph, msph); UP(mbox, mbox); UP(mtor, mtor);
     UP(mats, mats); UP(bloom, bloom); UP(bvh, bvh); UP(bvh_prims, bvh_prims); UP(always, always);
+    UP(snodes, snodes); UP(srecs, srecs); UP(always2, always2);
 #undef UP
     S.n_sph = fw.counts[0]; S.n_cube = fw.counts[1]; S.n_tri = fw.counts[2]; S.n_plane = fw.counts[3]; S.n_para = fw.counts[4];
     S.n_msph = fw.counts[5]; S.n_mbox = fw.counts[6]; S.n_mtor = fw.counts[7];
@@ -597,6 +489,9 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     S.off_msph = fw.offsets[5]; S.off_mbox = fw.offsets[6]; S.off_mtor = fw.offsets[7]; S.n_total = fw.offsets[8];
     S.n_bvh_nodes = (uint32_t)fw.bvh.size();
     S.n_always = (uint32_t)fw.always.size();
+    S.n_snodes = (uint32_t)fw.snodes.size(); S.n_srecs = (uint32_t)fw.srecs.size(); S.n_always2 = (uint32_t)fw.always2.size();
+    const size_t lds = fw.snodes.size() * sizeof(OmSkipNode) + fw.srecs.size() * sizeof(OmAffineTest);
+    S.lds_bytes = lds <= kLdsBudget ? (uint32_t)(lds < 16 ? 16 : lds) : 0u;
     OM_HIP(c, hipStreamSynchronize(c->stream));
     c->have_world = true;
     return OM_OK;
@@ -604,7 +499,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
 
 om_status om_set_kernel(om_ctx* c, int32_t k) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
-    if (k < OM_KERNEL_AUTO || k > OM_KERNEL_BVH) return set_err(c, OM_ERR_INVALID, "om_set_kernel: unknown kernel");
+    if (k < OM_KERNEL_AUTO || k > OM_KERNEL_SBVH) return set_err(c, OM_ERR_INVALID, "om_set_kernel: unknown kernel");
     c->kernel = k;
     return OM_OK;
 }
@@ -656,6 +551,20 @@ om_status om_get_counters(om_ctx* c, om_counters* out) {
     OM_HIP(c, hipMemcpy(h, c->counters.p, sizeof(h), hipMemcpyDeviceToHost));
     out->samples = h[OMC_SAMPLES]; out->segments = h[OMC_SEGMENTS]; out->prim_tests = h[OMC_PRIM_TESTS];
     out->pre_tests = h[OMC_PRE_TESTS]; out->march_steps = h[OMC_MARCH]; out->credited = h[OMC_CREDITED];
+    return OM_OK;
+}
+
+om_status om_set_pipeline(om_ctx* c, int32_t pipeline) {
+    if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
+    if (pipeline != OM_PIPELINE_MEGAKERNEL && pipeline != OM_PIPELINE_WAVEFRONT)
+        return set_err(c, OM_ERR_INVALID, "om_set_pipeline: unknown pipeline");
+    c->pipeline = pipeline;
+    return OM_OK;
+}
+
+om_status om_set_counting(om_ctx* c, int32_t enable) {
+    if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
+    c->count_work = enable != 0;
     return OM_OK;
 }
 

@@ -1,0 +1,290 @@
+// om_trace.h — closest-hit query over the frozen world (hits.rs:270-365) and the
+// HitRecord of the winner; shared by the megakernel (om_render.hip) and the
+// wavefront pipeline (om_wavefront.hip).
+#pragma once
+#include "om_device.h"
+#include "om_layout.h"
+
+namespace omd {
+
+// Work counters (om_counters); compiled out (COUNT=false) of the production kernels so
+// they cost no registers — the bench counts work in a separate, identical launch.
+template <bool COUNT>
+struct WorkT {
+    uint32_t prim = 0, pre = 0, march = 0;
+    __device__ __forceinline__ void add_prim() { if (COUNT) prim++; }
+    __device__ __forceinline__ void add_pre(uint32_t k = 1) { if (COUNT) pre += k; }
+    __device__ __forceinline__ void add_march() { if (COUNT) march++; }
+};
+
+// Exact test of global primitive gi with the brute-force acceptance (root <= tmax).
+__device__ __forceinline__ bool test_prim(const OmSceneDev& S, uint32_t gi, F3 o, F3 d, float tmin, float tmax, float& t) {
+    if (gi < S.off_cube) return sphere_root(S.sph_test[gi], o, d, tmin, tmax, t);
+    if (gi < S.off_tri) { int ax; return cube_root(S.cube_test[gi - S.off_cube], o, d, tmin, tmax, t, ax); }
+    float ndd;
+    if (gi < S.off_plane) return bary_root<true>(S.tri[gi - S.off_tri], o, d, tmin, tmax, t, ndd);
+    if (gi < S.off_para) return plane_root(S.plane[gi - S.off_plane], o, d, tmin, tmax, t, ndd);
+    return bary_root<false>(S.para[gi - S.off_para], o, d, tmin, tmax, t, ndd);
+}
+
+// Reference order brute force: FrozenHittableList::hit traced section (hits.rs:272-285).
+// CULL: skip spheres whose conservative bounding sphere proves the exact test
+// would return None — the accepted sequence is unchanged.
+template <bool CULL, class Wk>
+__device__ __forceinline__ int traced_brute(const OmSceneDev& S, F3 o, F3 d, float tmin, float& closest, Wk& w) {
+    int best = -1;
+    float t;
+    for (uint32_t i = 0; i < S.n_sph; ++i) {
+        if (CULL) {
+            const OmBound B = S.sph_bound[i];
+            const float ocx = o.x - B.c[0], ocy = o.y - B.c[1], ocz = o.z - B.c[2];
+            const float b = ocx * d.x + ocy * d.y + ocz * d.z;
+            const float px = ocx - b * d.x, py = ocy - b * d.y, pz = ocz - b * d.z;
+            const float q = px * px + py * py + pz * pz;
+            w.add_pre();
+            // every comparison is false for NaN -> the exact test decides
+            if (q > B.r * B.r || -b + B.r < tmin || -b - B.r > closest) continue;
+        }
+        w.add_prim();
+        if (sphere_root(S.sph_test[i], o, d, tmin, closest, t)) { closest = t; best = (int)i; }
+    }
+    for (uint32_t i = 0; i < S.n_cube; ++i) {
+        int ax; w.add_prim();
+        if (cube_root(S.cube_test[i], o, d, tmin, closest, t, ax)) { closest = t; best = (int)(S.off_cube + i); }
+    }
+    float ndd;
+    for (uint32_t i = 0; i < S.n_tri; ++i) {
+        w.add_prim();
+        if (bary_root<true>(S.tri[i], o, d, tmin, closest, t, ndd)) { closest = t; best = (int)(S.off_tri + i); }
+    }
+    for (uint32_t i = 0; i < S.n_plane; ++i) {
+        w.add_prim();
+        if (plane_root(S.plane[i], o, d, tmin, closest, t, ndd)) { closest = t; best = (int)(S.off_plane + i); }
+    }
+    for (uint32_t i = 0; i < S.n_para; ++i) {
+        w.add_prim();
+        if (bary_root<false>(S.para[i], o, d, tmin, closest, t, ndd)) { closest = t; best = (int)(S.off_para + i); }
+    }
+    return best;
+}
+
+// BVH traversal with the brute-force tie rule: the reference keeps the smallest
+// accepted root and, on equal roots, the later object in type order.
+template <class Wk>
+__device__ __forceinline__ void offer(const OmSceneDev& S, uint32_t gi, F3 o, F3 d, float tmin, float& closest, int& best, Wk& w) {
+    float t;
+    w.add_prim();
+    if (test_prim(S, gi, o, d, tmin, closest, t)) {
+        if (t < closest || (int)gi > best) { closest = t; best = (int)gi; }
+    }
+}
+
+template <class Wk>
+__device__ __forceinline__ int traced_bvh(const OmSceneDev& S, F3 o, F3 d, float tmin, float& closest, Wk& w) {
+    // Non-finite rays take the reference loop (NaN roots are accepted there).
+    if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return traced_brute<false, Wk>(S, o, d, tmin, closest, w);
+    int best = -1;
+    for (uint32_t k = 0; k < S.n_always; ++k) offer(S, S.always[k], o, d, tmin, closest, best, w);
+    if (S.n_bvh_nodes == 0) return best;
+    const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+    const float t_lo = tmin * 0.5f - 1e-3f;
+    uint32_t stack[64];
+    int sp = 0;
+    uint32_t node = 0;
+    for (;;) {
+        const OmBvhNode N = S.bvh[node];
+        if (N.left < 0) {
+            const uint32_t first = (uint32_t)(-N.left - 1), cnt = (uint32_t)N.right;
+            for (uint32_t k = 0; k < cnt; ++k) offer(S, S.bvh_prims[first + k], o, d, tmin, closest, best, w);
+        } else {
+            const OmBvhNode L = S.bvh[N.left], R = S.bvh[N.right];
+            w.add_pre(2);
+            // Slab tests on inflated boxes, (lo - o) * (1/d): a zero direction component
+            // gives +-inf (correct containment) or NaN (dropped by fminf/fmaxf = unconstrained).
+            const float t_hi = closest * 1.0001f + 1e-3f;
+            float x0 = (L.lo[0] - o.x) * ix, x1 = (L.hi[0] - o.x) * ix;
+            float y0 = (L.lo[1] - o.y) * iy, y1 = (L.hi[1] - o.y) * iy;
+            float z0 = (L.lo[2] - o.z) * iz, z1 = (L.hi[2] - o.z) * iz;
+            const float ln = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+            const float lf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+            x0 = (R.lo[0] - o.x) * ix; x1 = (R.hi[0] - o.x) * ix;
+            y0 = (R.lo[1] - o.y) * iy; y1 = (R.hi[1] - o.y) * iy;
+            z0 = (R.lo[2] - o.z) * iz; z1 = (R.hi[2] - o.z) * iz;
+            const float rn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+            const float rf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+            const bool hl = ln <= lf, hr = rn <= rf;
+            if (hl && hr) {
+                const bool left_first = ln <= rn;
+                stack[sp++] = left_first ? (uint32_t)N.right : (uint32_t)N.left;
+                node = left_first ? (uint32_t)N.left : (uint32_t)N.right;
+                continue;
+            }
+            if (hl) { node = (uint32_t)N.left; continue; }
+            if (hr) { node = (uint32_t)N.right; continue; }
+        }
+        if (sp == 0) break;
+        node = stack[--sp];
+    }
+    return best;
+}
+
+// Stackless BVH traversal.  Nodes are visited in depth-first
+// order: box hit -> next node (internal) or the leaf's records then `skip`; miss ->
+// `skip`.  No per-lane stack (no scratch), one 32-B node read per step.  The box test
+// only decides which exact tests run, so it may use FMA (it never touches output bits):
+// boxes are inflated far beyond its rounding, the direction is kept away from 0 so
+// every slab value is finite, and NaN compares fall through to "visit".
+// NODES/RECS point into LDS (staged once per workgroup) or into global memory.
+template <class Wk>
+__device__ __forceinline__ int traced_sbvh(const OmSceneDev& S, const OmSkipNode* nodes, const OmAffineTest* recs,
+                                           F3 o, F3 d, float tmin, float& closest, Wk& w) {
+    if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return traced_brute<false, Wk>(S, o, d, tmin, closest, w);
+    int best = -1;
+    for (uint32_t k = 0; k < S.n_always2; ++k) offer(S, S.always2[k], o, d, tmin, closest, best, w);
+    const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
+    const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
+    const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
+    const float t_lo = tmin * 0.5f - 1e-3f;
+    const uint32_t n = S.n_snodes;
+    uint32_t node = 0;
+    while (node < n) {
+        const OmSkipNode N = nodes[node];
+        w.add_pre();
+        const float t_hi = closest * 1.0001f + 1e-3f;
+        const float x0 = __builtin_fmaf(N.lo[0], ix, nox), x1 = __builtin_fmaf(N.hi[0], ix, nox);
+        const float y0 = __builtin_fmaf(N.lo[1], iy, noy), y1 = __builtin_fmaf(N.hi[1], iy, noy);
+        const float z0 = __builtin_fmaf(N.lo[2], iz, noz), z1 = __builtin_fmaf(N.hi[2], iz, noz);
+        const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+        const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        if (!(tn > tf)) {
+            if (N.leaf == 0xFFFFFFFFu) { node++; continue; }
+            const uint32_t first = N.leaf >> 8, cnt = N.leaf & 255u;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const OmAffineTest R = recs[first + k];
+                uint32_t tag;
+                __builtin_memcpy(&tag, &R.pad, 4);
+                const uint32_t gi = tag & 0x7FFFFFFFu;
+                float t;
+                int ax;
+                w.add_prim();
+                const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root(R, o, d, tmin, closest, t);
+                if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
+            }
+        }
+        node = N.skip;
+    }
+    return best;
+}
+
+// unstuck (hits.rs:336-365) + sphere-tracing loop (hits.rs:287-333).
+// Returns the marched winner's global index or -1; `t` receives the hit t.
+template <class Wk>
+__device__ __forceinline__ int march(const OmSceneDev& S, F3 o, F3 d, float tmin, float tmax, float closest,
+                                     uint32_t steps, float& t_hit, Wk& w) {
+    const float HIT = 0.001f;
+    // nearest marched object at r.at(tmin), strict '<' (first minimum wins)
+    F3 p = at(o, d, tmin);
+    float dist = INFINITY; int kind = -1; uint32_t idx = 0;
+    for (uint32_t i = 0; i < S.n_msph; ++i) { const float v = fabsf(msphere_sdf(S.msph[i], p)); if (v < dist) { dist = v; kind = 0; idx = i; } }
+    for (uint32_t i = 0; i < S.n_mbox; ++i) { const float v = fabsf(mbox_sdf(S.mbox[i], p)); if (v < dist) { dist = v; kind = 1; idx = i; } }
+    for (uint32_t i = 0; i < S.n_mtor; ++i) { const float v = fabsf(mtorus_sdf(S.mtor[i], p)); if (v < dist) { dist = v; kind = 2; idx = i; } }
+    if (kind < 0) return -1;                                                   // hits.rs:359
+    float t = tmin;
+    float aux = dist;
+    uint32_t guard = 0;
+    while (aux < HIT && guard++ < (1u << 22)) {                                // hits.rs:360-363 (+ safety cap)
+        t += HIT / 2.0f;
+        const F3 q = at(o, d, t);
+        aux = kind == 0 ? fabsf(msphere_sdf(S.msph[idx], q)) : kind == 1 ? fabsf(mbox_sdf(S.mbox[idx], q)) : fabsf(mtorus_sdf(S.mtor[idx], q));
+    }
+    uint32_t iters = steps;
+    while (t < tmax && t < closest && iters > 0) {                            // hits.rs:294
+        iters -= 1;
+        w.add_march();
+        p = at(o, d, t);
+        float best = INFINITY; int bk = -1; uint32_t bi = 0;
+        for (uint32_t i = 0; i < S.n_msph; ++i) { const float v = fabsf(msphere_sdf(S.msph[i], p)); if (v < best) { best = v; bk = 0; bi = i; } }
+        for (uint32_t i = 0; i < S.n_mbox; ++i) { const float v = fabsf(mbox_sdf(S.mbox[i], p)); if (v < best) { best = v; bk = 1; bi = i; } }
+        for (uint32_t i = 0; i < S.n_mtor; ++i) { const float v = fabsf(mtorus_sdf(S.mtor[i], p)); if (v < best) { best = v; bk = 2; bi = i; } }
+        if (bk < 0) return -1;                                                 // hits.rs:323
+        if (best < HIT) {                                                      // hits.rs:325-327
+            t_hit = t;
+            return (int)(bk == 0 ? S.off_msph + bi : bk == 1 ? S.off_mbox + bi : S.off_mtor + bi);
+        }
+        t += best;                                                             // hits.rs:330
+    }
+    return -1;
+}
+
+// Build the HitRecord of the winner (point, normal) — the winner's own exact
+// test re-run with tmax = its root reproduces the same root bit for bit.
+__device__ __forceinline__ void finalize(const OmSceneDev& S, int gi, F3 o, F3 d, float tmin, float t, F3& point, F3& normal) {
+    const uint32_t g = (uint32_t)gi;
+    if (g < S.off_tri) {                                                       // Sphere / Cube
+        const bool cube = g >= S.off_cube;
+        const OmAffineTest& T = cube ? S.cube_test[g - S.off_cube] : S.sph_test[g];
+        const OmAffineHit& H = cube ? S.cube_hit[g - S.off_cube] : S.sph_hit[g];
+        const F3 lo = xform_p(T.w2l, o), ld = xform_v(T.w2l, T.dz, d);
+        const F3 lp = at(lo, ld, t);
+        point = xform_p(H.l2w, lp);
+        if (!cube) {
+            normal = unit(xform_v(H.l2w, H.lz, lp));                           // traced.rs:59
+        } else {
+            float r; int ax = 0;
+            cube_root(T, o, d, tmin, t, r, ax);
+            // traced.rs:293-296: axis * copysign(1, p[idx]); normal NOT normalised
+            const float comp = ax == 0 ? lp.x : (ax == 1 ? lp.y : lp.z);
+            const float s = copysignf(1.0f, comp);
+            const F3 ln = f3((ax == 0 ? 1.0f : 0.0f) * s, (ax == 1 ? 1.0f : 0.0f) * s, (ax == 2 ? 1.0f : 0.0f) * s);
+            normal = xform_v(H.l2w, H.lz, ln);
+        }
+        return;
+    }
+    if (g < S.off_msph) {                                                      // plane / barycentric
+        F3 n, c;
+        if (g < S.off_plane) { n = ld3(S.tri[g - S.off_tri].uxv); c = ld3(S.tri[g - S.off_tri].origin); }
+        else if (g < S.off_para) { n = ld3(S.plane[g - S.off_plane].normal); c = ld3(S.plane[g - S.off_plane].center); }
+        else { n = ld3(S.para[g - S.off_para].uxv); c = ld3(S.para[g - S.off_para].origin); }
+        float r, ndd;
+        plane_isect(n, c, o, d, r, ndd);
+        point = at(o, d, t);
+        normal = scl(n, copysignf(1.0f, -ndd));                                // traced.rs:101-103
+        return;
+    }
+    point = at(o, d, t);                                                       // marched (hits.rs:326)
+    if (g < S.off_mbox) normal = msphere_normal(S.msph[g - S.off_msph], point);
+    else if (g < S.off_mtor) normal = mbox_normal(S.mbox[g - S.off_mbox], point);
+    else normal = mtorus_normal(S.mtor[g - S.off_mtor], point);
+}
+
+}  // namespace omd
+
+namespace omd {
+
+// render_thread.rs:183-192 + Camera::get_ray (camera.rs:60-65): the primary ray of
+// sample s of pixel (i_f, j_f); g is the path's fresh om-rng stream.
+__device__ __forceinline__ void gen_camera_ray(const OmCamDev& C, const OmParamsDev& P, const float2* jitter,
+                                               float i_f, float j_f, uint32_t s, Rng& g, F3& o, F3& d) {
+    const float2 jt = jitter[s];
+    const float i_rand = (g.next() + jt.x) / 2.0f;
+    const float j_rand = (g.next() + jt.y) / 2.0f;
+    const float u = (i_f + i_rand) / P.wf_m1;
+    const float v = 1.0f - (j_f + j_rand) / P.hf_m1;
+    float dx, dy;
+    for (;;) {                                                     // rand_in_unit_disc vec3.rs:108-113
+        dx = g.range(-1.0f, 1.0f);
+        dy = g.range(-1.0f, 1.0f);
+        if (dx * dx + dy * dy < 1.0f) break;
+    }
+    const float rlx = dx * C.lens_radius, rly = dy * C.lens_radius;
+    const F3 off = f3(C.u[0] * rlx + C.v[0] * rly, C.u[1] * rlx + C.v[1] * rly, C.u[2] * rlx + C.v[2] * rly);
+    // uv_to_dir . (u, v, 0, 1): ((H*u + V*v) + 0*0) + D*1
+    const F3 dir = f3((C.horizontal[0] * u + C.vertical[0] * v) + 0.0f * 0.0f + C.llc_minus_origin[0],
+                      (C.horizontal[1] * u + C.vertical[1] * v) + 0.0f * 0.0f + C.llc_minus_origin[1],
+                      (C.horizontal[2] * u + C.vertical[2] * v) + 0.0f * 0.0f + C.llc_minus_origin[2]);
+    o = add(ld3(C.origin), off);
+    d = unit(unit(sub(dir, off)));                                 // camera.rs:64 + ray.rs:12
+}
+
+}  // namespace omd

@@ -1,0 +1,43 @@
+// om_wavefront.h — host interface of the wavefront pipeline.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/ottomarcher.h"
+#include "om_layout.h"
+
+namespace omw {
+
+// Device work buffers of one context; grown on demand, never shrunk.
+struct Buffers {
+    uint64_t cap = 0;            // paths per batch
+    float4* q[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};  // ping-pong queues: o|depthf, d|first_id, cur|seg
+    uint4* qr[2] = {nullptr, nullptr};   // rng lo, rng hi, path slot, pad
+    float2* hits = nullptr;      // t, gi (bits)
+    float4* res = nullptr;       // colour.xyz, depth
+    uint32_t* res_id = nullptr;  // obj id (0xFFFFFFFF = no sample)
+    uint32_t* counts = nullptr;  // per bounce, per queue segment: live rays
+    uint32_t counts_n = 0;       // words allocated
+    void release();
+};
+
+struct Launch {
+    OmSceneDev S;
+    OmCamDev C;
+    OmParamsDev P;
+    const float2* jitter;
+    om_pixel_stats* stats;
+    const uint32_t* pixels;      // device list of row-major pixel indices (tile order)
+    uint32_t n_pixels;
+    bool stats_by_pixel;         // stats[pixel] (full frame) instead of stats[k]
+    unsigned long long* counters;
+    bool count;
+    int trace_mode;              // closest-hit kernel variant (om_render.hip MODE_*)
+};
+
+// Renders P.sample_count samples of every listed pixel; returns 0 or a HIP error text.
+hipError_t render(Buffers& B, const Launch& L, hipStream_t stream, std::string& err);
+
+}  // namespace omw

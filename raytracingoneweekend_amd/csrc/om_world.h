@@ -36,6 +36,9 @@ struct FrozenWorld {
     std::vector<OmBvhNode> bvh;
     std::vector<uint32_t> bvh_prims;   // global indices
     std::vector<uint32_t> always;      // global indices tested outside the BVH
+    std::vector<OmSkipNode> snodes;    // stackless BVH (affine prims only)
+    std::vector<OmAffineTest> srecs;   // its records in leaf order
+    std::vector<uint32_t> always2;     // prims outside the stackless BVH
     uint32_t counts[8];
     uint32_t offsets[9];               // global index offset per kind, offsets[8] = total
 };

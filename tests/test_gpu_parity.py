@@ -8,12 +8,16 @@ from scenes_common import compare_stats, kitchen_sink
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["brute", "culled", "bvh"]
+KERNELS = ["brute", "culled", "bvh", "sbvh"]
+PIPELINES = ["megakernel", "wavefront"]
+COMBOS = [(k, p) for p in PIPELINES for k in KERNELS]
 
 
 def _render_both(om, O, world, oworld, cam, ocam, W, H, spp, kernel, seed=3, max_depth=50, adaptive=False,
-                 sample_count=None, march_steps=1024):
-    frozen = world.freeze(cam, kernel=kernel)
+                 sample_count=None, march_steps=1024, pipeline="wavefront"):
+    if isinstance(kernel, tuple):
+        kernel, pipeline = kernel
+    frozen = world.freeze(cam, kernel=kernel, pipeline=pipeline)
     pix = om.PixelsBox.new(W * H)
     om.render(cam, frozen, max_depth, 0.001, 100.0, spp, W, H, pix, seed=seed, adaptive=adaptive,
               sample_count=sample_count, march_steps=march_steps)
@@ -23,7 +27,7 @@ def _render_both(om, O, world, oworld, cam, ocam, W, H, spp, kernel, seed=3, max
     return pix.pixels, exp, frozen
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", COMBOS)
 def test_traced_scene_bit_exact(om, oracle, kernel):
     W, H, SPP = 64, 40, 6
     got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED), oracle.random_scene(0x5EED),
@@ -33,7 +37,7 @@ def test_traced_scene_bit_exact(om, oracle, kernel):
     assert (got["n"] == SPP).all()
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", COMBOS)
 def test_full_scene_with_torus_bit_exact(om, oracle, kernel):
     W, H, SPP = 40, 28, 3
     got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED, with_torus=True),
@@ -43,7 +47,7 @@ def test_full_scene_with_torus_bit_exact(om, oracle, kernel):
     assert nb == 0, msg
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", COMBOS)
 def test_kitchen_sink_every_primitive_bit_exact(om, oracle, kernel):
     W, H, SPP = 48, 32, 4
     w, ow, cam, ocam = kitchen_sink(om, oracle)
@@ -52,29 +56,32 @@ def test_kitchen_sink_every_primitive_bit_exact(om, oracle, kernel):
     assert nb == 0, msg
 
 
-def test_marched_scene_bit_exact(om, oracle):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_marched_scene_bit_exact(om, oracle, pipeline):
     W, H, SPP = 32, 20, 2
     got, exp, _ = _render_both(om, oracle, om.marched_scene(), oracle.marched_scene(), om.default_camera(W / H),
-                               oracle.default_camera(W / H), W, H, SPP, "auto", march_steps=256)
+                               oracle.default_camera(W / H), W, H, SPP, "auto", march_steps=256, pipeline=pipeline)
     nb, msg = compare_stats(got, exp, "S-marched")
     assert nb == 0, msg
 
 
-def test_adaptive_retirement_bit_exact(om, oracle):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_adaptive_retirement_bit_exact(om, oracle, pipeline):
     W, H, SPP = 32, 24, 24
     got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED), oracle.random_scene(0x5EED),
                                om.default_camera(W / H), oracle.default_camera(W / H), W, H, SPP, "auto",
-                               adaptive=True)
+                               adaptive=True, pipeline=pipeline)
     nb, msg = compare_stats(got, exp, "adaptive")
     assert nb == 0, msg
     assert got["n"].min() < SPP  # some pixels (sky) retired early, like the reference
 
 
-def test_progressive_calls_equal_single_call(om):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_progressive_calls_equal_single_call(om, pipeline):
     W, H = 40, 24
     world = om.random_scene(0x5EED)
     cam = om.default_camera(W / H)
-    fz = world.freeze(cam)
+    fz = world.freeze(cam, pipeline=pipeline)
     a = om.PixelsBox.new(W * H)
     om.render(cam, fz, 50, 0.001, 100.0, 8, W, H, a, seed=5)
     b = om.PixelsBox.new(W * H)
@@ -84,35 +91,84 @@ def test_progressive_calls_equal_single_call(om):
     assert nb == 0, msg
 
 
-def test_shallow_depth_and_exhaustion(om, oracle):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_shallow_depth_and_exhaustion(om, oracle, pipeline):
     # max_depth 1 and 0: every hit path ends with -Color::ZERO (render_thread.rs:142)
     W, H = 24, 16
     for depth in (0, 1, 2):
         got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED), oracle.random_scene(0x5EED),
                                    om.default_camera(W / H), oracle.default_camera(W / H), W, H, 2, "auto",
-                                   max_depth=depth)
+                                   max_depth=depth, pipeline=pipeline)
         nb, msg = compare_stats(got, exp, f"depth{depth}")
         assert nb == 0, msg
 
 
-def test_ten_k_scene_bvh_bit_exact(om, oracle):
+@pytest.mark.parametrize("kernel", [("bvh", "megakernel"), ("sbvh", "megakernel"), ("bvh", "wavefront"),
+                                    ("sbvh", "wavefront")])
+def test_ten_k_scene_bvh_bit_exact(om, oracle, kernel):
     W, H, SPP = 32, 18, 2
     got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED, grid_half=50, extras=False),
                                oracle.random_scene(0x5EED, grid_half=50, extras=False),
-                               om.default_camera(W / H), oracle.default_camera(W / H), W, H, SPP, "bvh")
+                               om.default_camera(W / H), oracle.default_camera(W / H), W, H, SPP, kernel)
     nb, msg = compare_stats(got, exp, "S-10k")
     assert nb == 0, msg
 
 
-def test_counters_consistent(om):
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_counters_consistent(om, pipeline):
     W, H, SPP = 32, 16, 4
     world = om.random_scene(0x5EED)
     cam = om.default_camera(W / H)
     for k in KERNELS:
-        fz = world.freeze(cam, kernel=k)
+        fz = world.freeze(cam, kernel=k, pipeline=pipeline)
         pix = om.PixelsBox.new(W * H)
         c = om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=2)
         assert c["samples"] == W * H * SPP
         assert c["segments"] >= c["samples"]
         if k == "brute":
             assert c["prim_tests"] == c["segments"] * 485
+
+
+@pytest.mark.parametrize("kernel", COMBOS)
+def test_counting_build_is_bit_identical(om, kernel):
+    from raytracingoneweekend_amd import _lib as L
+    W, H, SPP = 48, 32, 3
+    world = om.random_scene(0x5EED, with_torus=True)
+    cam = om.default_camera(W / H)
+    out = []
+    for count in (1, 0):
+        fz = world.freeze(cam, kernel=kernel[0], pipeline=kernel[1])
+        L.check(L.lib.om_set_counting(fz.ctx, count), fz.ctx)
+        pix = om.PixelsBox.new(W * H)
+        om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=4)
+        out.append(pix.pixels.copy())
+    nb, msg = compare_stats(out[1], out[0], f"count/{kernel}")
+    assert nb == 0, msg
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_pixel_list_shard_equals_full_frame(om, kernel):
+    """om_render_device_pixels over rank shards (wavefront) == one full-frame render."""
+    import ctypes as C
+    import torch
+    from raytracingoneweekend_amd import _lib as L
+    from raytracingoneweekend_amd import shard
+    W, H, SPP = 40, 24, 3
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    full = om.PixelsBox.new(W * H)
+    fz = world.freeze(cam, kernel=kernel)
+    om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, full, seed=6)
+    shards = []
+    p = om.make_params(50, 0.001, 100.0, SPP, W, H, seed=6)
+    for r in range(3):
+        pix = shard.tile_pixels(W, H, r, 3)
+        dpix = torch.from_numpy(pix.view(np.int32)).cuda()
+        st = torch.zeros(pix.size * 40, dtype=torch.uint8, device="cuda")
+        L.check(L.lib.om_render_device_pixels(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()),
+                                              C.c_void_p(dpix.data_ptr()), pix.size, None), fz.ctx)
+        torch.cuda.synchronize()
+        shards.append(st.cpu().numpy())
+    frame = shard.assemble(W, H, shards)
+    nb, msg = compare_stats(frame, full.pixels, f"shards/{kernel}")
+    assert nb == 0, msg
