@@ -77,7 +77,10 @@ struct Builder {
     }
 
     // builds items[begin,end) ; returns node index
-    uint32_t build(uint32_t begin, uint32_t end) {
+    // SAH down to depth kSahDepth, then median splits: depth <= kSahDepth + log2(n)
+    // keeps every tree within the traversal stacks (24 entries, 64 for the global BVH).
+    static constexpr uint32_t kSahDepth = 10;
+    uint32_t build(uint32_t begin, uint32_t end, uint32_t depth = 0) {
         Box bb; bb.empty(); Box cb; cb.empty();
         for (uint32_t i = begin; i < end; ++i) { bb.grow(items[i].b); cb.grow_pt(items[i].c); }
         const uint32_t node = emit(bb);
@@ -116,16 +119,16 @@ struct Builder {
         }
         const double leaf_cost = bb.area() * count;
         const double trav = 1.0 * bb.area();  // traversal cost relative to one primitive test
-        if (best_axis < 0) {
-            if (count <= 8) return make_leaf();
+        if (best_axis < 0 || depth >= kSahDepth) {
+            if (count <= 4 || (best_axis < 0 && count <= 8)) return make_leaf();
             // degenerate centroids: median split on the longest box axis
             int ax = 0;
             for (int k = 1; k < 3; ++k) if (bb.hi[k] - bb.lo[k] > bb.hi[ax] - bb.lo[ax]) ax = k;
             std::nth_element(items.begin() + begin, items.begin() + begin + count / 2, items.begin() + end,
                              [ax](const Item& x, const Item& y) { return x.c[ax] < y.c[ax]; });
             const uint32_t mid = begin + count / 2;
-            const uint32_t l = build(begin, mid);
-            const uint32_t r = build(mid, end);
+            const uint32_t l = build(begin, mid, depth + 1);
+            const uint32_t r = build(mid, end, depth + 1);
             nodes[node].left = (int32_t)l; nodes[node].right = (int32_t)r;
             return node;
         }
@@ -139,8 +142,8 @@ struct Builder {
         });
         uint32_t mid = (uint32_t)(mid_it - items.begin());
         if (mid == begin || mid == end) mid = begin + count / 2;
-        const uint32_t l = build(begin, mid);
-        const uint32_t r = build(mid, end);
+        const uint32_t l = build(begin, mid, depth + 1);
+        const uint32_t r = build(mid, end, depth + 1);
         nodes[node].left = (int32_t)l; nodes[node].right = (int32_t)r;
         return node;
     }
@@ -201,8 +204,10 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     if (b.items.empty()) return;
     const uint32_t root = b.build(0, (uint32_t)b.items.size());
     // depth-first re-emission with skip links
+    std::vector<uint32_t> leaf_first(b.nodes.size(), 0);
     struct Emit {
         const Builder& b; const FrozenWorld& fw; std::vector<OmSkipNode>& out; std::vector<OmAffineTest>& recs;
+        std::vector<uint32_t>& leaf_first;
         void rec(uint32_t n) {
             const OmBvhNode& src = b.nodes[n];
             const uint32_t idx = (uint32_t)out.size();
@@ -213,6 +218,7 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
             if (src.left < 0) {
                 const uint32_t first = (uint32_t)(-src.left - 1), cnt = (uint32_t)src.right;
                 out[idx].leaf = ((uint32_t)recs.size() << 8) | cnt;
+                leaf_first[n] = (uint32_t)recs.size();
                 for (uint32_t k = 0; k < cnt; ++k) {
                     const uint32_t gi = b.order[first + k];
                     const bool cube = gi >= fw.offsets[K_CUBE];
@@ -227,8 +233,58 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
             }
             out[idx].skip = (uint32_t)out.size();
         }
-    } e{b, fw, fw.snodes, fw.srecs};
+    } e{b, fw, fw.snodes, fw.srecs, leaf_first};
     e.rec(root);
+
+    // compressed BVH2: both child boxes in the parent (one 64-B read per visit)
+    struct Emit2 {
+        const Builder& b; const std::vector<uint32_t>& leaf_first; std::vector<OmBvh2Node>& out;
+        std::vector<uint32_t>& leaves;
+        uint32_t code(uint32_t c) {
+            const OmBvhNode& n = b.nodes[c];
+            if (n.left < 0) {
+                leaves.push_back((leaf_first[c] << 8) | (uint32_t)n.right);
+                return OM_LEAF | (uint32_t)(leaves.size() - 1);
+            }
+            return rec(c);
+        }
+        uint32_t rec(uint32_t n) {
+            const uint32_t idx = (uint32_t)out.size();
+            out.push_back(OmBvh2Node{});
+            const OmBvhNode& src = b.nodes[n];
+            const OmBvhNode& L = b.nodes[(uint32_t)src.left];
+            const OmBvhNode& R = b.nodes[(uint32_t)src.right];
+            OmBvh2Node o{};
+            for (int i = 0; i < 3; ++i) { o.lo0[i] = L.lo[i]; o.hi0[i] = L.hi[i]; o.lo1[i] = R.lo[i]; o.hi1[i] = R.hi[i]; }
+            o.c0 = code((uint32_t)src.left);
+            o.c1 = code((uint32_t)src.right);
+            out[idx] = o;
+            return idx;
+        }
+    } e2{b, leaf_first, fw.b2nodes, fw.b2leaves};
+    fw.b2nodes.clear();
+    fw.b2leaves.clear();
+    if (b.nodes[root].left < 0) {            // a single leaf: one node, second child an empty leaf
+        OmBvh2Node o{};
+        for (int i = 0; i < 3; ++i) {
+            o.lo0[i] = b.nodes[root].lo[i]; o.hi0[i] = b.nodes[root].hi[i];
+            o.lo1[i] = INFINITY; o.hi1[i] = -INFINITY;
+        }
+        fw.b2leaves.push_back((leaf_first[root] << 8) | (uint32_t)b.nodes[root].right);
+        fw.b2leaves.push_back(0u);
+        o.c0 = OM_LEAF | 0u;
+        o.c1 = OM_LEAF | 1u;
+        fw.b2nodes.push_back(o);
+    } else {
+        e2.rec(root);
+    }
+    // depth of the compressed tree (the traversal's stack bound)
+    std::vector<uint32_t> depth(fw.b2nodes.size(), 1);
+    fw.b2_depth = 1;
+    for (uint32_t i = 0; i < fw.b2nodes.size(); ++i) {   // parents precede children (DFS)
+        for (uint32_t c : {fw.b2nodes[i].c0, fw.b2nodes[i].c1})
+            if (!(c & OM_LEAF)) { depth[c] = depth[i] + 1; fw.b2_depth = std::max(fw.b2_depth, depth[c]); }
+    }
 }
 
 }  // namespace om

@@ -97,6 +97,22 @@ struct OM_ALIGN16 OmSkipNode {
     uint32_t leaf;
 };
 
+// Compressed binary BVH node (64 B): both child boxes live in the parent, so one
+// node read yields both slab tests.  child = 16-bit code: node index, or
+// OM_LEAF | leaf index; b2leaves[leaf] = (first_record << 8) | count (records =
+// srecs, leaf order).  The traversal stack holds these 16-bit codes.
+#define OM_LEAF 0x8000u
+struct OM_ALIGN16 OmBvh2Node {
+    float lo0[3];
+    uint32_t c0;
+    float hi0[3];
+    uint32_t pad0;
+    float lo1[3];
+    uint32_t c1;
+    float hi1[3];
+    uint32_t pad1;
+};
+
 // Device view of a frozen world (passed by value as a kernel argument).
 struct OmSceneDev {
     const OmAffineTest* sph_test; const OmAffineHit* sph_hit; const OmBound* sph_bound;
@@ -117,6 +133,11 @@ struct OmSceneDev {
     const OmSkipNode* snodes; const OmAffineTest* srecs; const uint32_t* always2;
     uint32_t n_snodes, n_srecs, n_always2;
     uint32_t lds_bytes;           // dynamic LDS the staged kernel needs (0 = scene too big: global path)
+    // compressed BVH2 over the same leaves/records as the stackless BVH
+    const OmBvh2Node* b2nodes;
+    const uint32_t* b2leaves;
+    uint32_t n_b2nodes, n_b2leaves;
+    uint32_t b2_lds_bytes;        // node bytes when they fit the LDS budget, else 0 (global nodes)
 };
 
 struct OmCamDev {

@@ -372,7 +372,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     }
     if (threads == 0) return OM_OK;
     int mode = c->kernel;
-    if (mode == OM_KERNEL_AUTO) mode = OM_KERNEL_SBVH;
+    if (mode == OM_KERNEL_AUTO) mode = c->pipeline == OM_PIPELINE_WAVEFRONT ? OM_KERNEL_BVH2 : OM_KERNEL_BVH;
     if (c->pipeline == OM_PIPELINE_WAVEFRONT) {
         omw::Launch L;
         L.S = c->scene; L.C = C; L.P = P;
@@ -381,7 +381,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         L.counters = (unsigned long long*)c->counters.p;
         L.count = c->count_work;
         L.trace_mode = mode == OM_KERNEL_BRUTE ? MODE_BRUTE : mode == OM_KERNEL_CULLED ? MODE_CULLED
-                     : mode == OM_KERNEL_BVH ? MODE_BVH : MODE_SBVH_LDS;
+                     : mode == OM_KERNEL_BVH ? MODE_BVH : mode == OM_KERNEL_BVH2 ? 6 : MODE_SBVH_LDS;
         if (dev_pixels) {
             L.pixels = dev_pixels; L.n_pixels = n_pixels; L.stats_by_pixel = false;
         } else {
@@ -481,7 +481,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     UP(tri, tri); UP(plane, plane); UP(para, para);
     UP(msph, msph); UP(mbox, mbox); UP(mtor, mtor);
     UP(mats, mats); UP(bloom, bloom); UP(bvh, bvh); UP(bvh_prims, bvh_prims); UP(always, always);
-    UP(snodes, snodes); UP(srecs, srecs); UP(always2, always2);
+    UP(snodes, snodes); UP(srecs, srecs); UP(always2, always2); UP(b2nodes, b2nodes); UP(b2leaves, b2leaves);
 #undef UP
     S.n_sph = fw.counts[0]; S.n_cube = fw.counts[1]; S.n_tri = fw.counts[2]; S.n_plane = fw.counts[3]; S.n_para = fw.counts[4];
     S.n_msph = fw.counts[5]; S.n_mbox = fw.counts[6]; S.n_mtor = fw.counts[7];
@@ -492,6 +492,15 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     S.n_snodes = (uint32_t)fw.snodes.size(); S.n_srecs = (uint32_t)fw.srecs.size(); S.n_always2 = (uint32_t)fw.always2.size();
     const size_t lds = fw.snodes.size() * sizeof(OmSkipNode) + fw.srecs.size() * sizeof(OmAffineTest);
     S.lds_bytes = lds <= kLdsBudget ? (uint32_t)(lds < 16 ? 16 : lds) : 0u;
+    // compressed BVH2: usable when its depth fits the 24-entry lane stack and node ids fit u16
+    // compressed BVH2: usable when node and leaf ids fit the 15-bit codes (a deeper
+    // tree than the lane stack falls back per ray to the reference loop)
+    const bool b2_ok = !fw.b2nodes.empty() && fw.b2nodes.size() < 32768u && fw.b2leaves.size() < 32768u &&
+                       fw.b2_depth <= 25u;   // 24-entry lane stack (om_wavefront.hip kStackDepth)
+    S.n_b2nodes = b2_ok ? (uint32_t)fw.b2nodes.size() : 0u;
+    S.n_b2leaves = b2_ok ? (uint32_t)fw.b2leaves.size() : 0u;
+    const size_t b2_bytes = fw.b2nodes.size() * sizeof(OmBvh2Node) + fw.b2leaves.size() * 4u;
+    S.b2_lds_bytes = (b2_ok && b2_bytes <= 40u * 1024u) ? (uint32_t)((b2_bytes + 15u) & ~(size_t)15u) : 0u;
     OM_HIP(c, hipStreamSynchronize(c->stream));
     c->have_world = true;
     return OM_OK;
@@ -499,7 +508,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
 
 om_status om_set_kernel(om_ctx* c, int32_t k) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
-    if (k < OM_KERNEL_AUTO || k > OM_KERNEL_SBVH) return set_err(c, OM_ERR_INVALID, "om_set_kernel: unknown kernel");
+    if (k < OM_KERNEL_AUTO || k > OM_KERNEL_BVH2) return set_err(c, OM_ERR_INVALID, "om_set_kernel: unknown kernel");
     c->kernel = k;
     return OM_OK;
 }

@@ -288,3 +288,92 @@ __device__ __forceinline__ void gen_camera_ray(const OmCamDev& C, const OmParams
 }
 
 }  // namespace omd
+
+namespace omd {
+
+// Compressed-BVH2 traversal: one 64-B node read gives both child
+// boxes; near child first, the far one pushed on a per-lane u16 stack that lives in
+// LDS (stk[level * STRIDE]) — no scratch memory.  Leaves hold only Sphere/Cube
+// records (everything else is in always2).  Box tests only choose which exact tests
+// run (FMA allowed, conservative, see traced_sbvh); the acceptance keeps the
+// brute-force tie rule, so the winner is bit-identical to hits.rs:274-285.
+// A stack overflow (tree deeper than DEPTH) falls back to the reference loop.
+// The reference loop's answer for a non-finite ray, in closed form (hits.rs:274-285):
+// every Sphere::hit accepts a NaN root (`disc < 0` and the range checks are all false
+// for NaN, traced.rs:46-55) and so does InfinitePlane::hit (traced.rs:108), while Cube
+// (is_solution false) and Barycentric (lambda checks false) reject.  The last accepted
+// object in type order wins: the last plane, else the last sphere; t is NaN.
+__device__ __forceinline__ int nonfinite_hit(const OmSceneDev& S, float& closest) {
+    if (S.n_plane) { closest = __int_as_float(0x7FC00000); return (int)(S.off_plane + S.n_plane - 1u); }
+    if (S.n_sph) { closest = __int_as_float(0x7FC00000); return (int)(S.n_sph - 1u); }
+    return -1;
+}
+
+template <int DEPTH, int STRIDE, class Wk>
+__device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node* nodes, const uint32_t* leaves, uint16_t* stk,
+                                           F3 o, F3 d, float tmin, float& closest, Wk& w) {
+    if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
+    int best = -1;
+    for (uint32_t k = 0; k < S.n_always2; ++k) offer(S, S.always2[k], o, d, tmin, closest, best, w);
+    const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
+    const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
+    const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
+    const float t_lo = tmin * 0.5f - 1e-3f;
+    const OmAffineTest* recs = S.srecs;
+    uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
+    int sp = 0;
+    bool overflow = false;
+    for (;;) {
+        if (cur & OM_LEAF) {                            // the single leaf site
+            const uint32_t lf = leaves[cur & (OM_LEAF - 1u)];
+            const uint32_t first = lf >> 8, cnt = lf & 255u;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const OmAffineTest R = recs[first + k];
+                uint32_t tag;
+                __builtin_memcpy(&tag, &R.pad, 4);
+                const uint32_t gi = tag & 0x7FFFFFFFu;
+                float t;
+                int ax;
+                w.add_prim();
+                const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root(R, o, d, tmin, closest, t);
+                if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
+            }
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * STRIDE];
+            continue;
+        }
+        const OmBvh2Node N = nodes[cur];
+        w.add_pre(2);
+        const float t_hi = closest * 1.0001f + 1e-3f;
+        float x0 = __builtin_fmaf(N.lo0[0], ix, nox), x1 = __builtin_fmaf(N.hi0[0], ix, nox);
+        float y0 = __builtin_fmaf(N.lo0[1], iy, noy), y1 = __builtin_fmaf(N.hi0[1], iy, noy);
+        float z0 = __builtin_fmaf(N.lo0[2], iz, noz), z1 = __builtin_fmaf(N.hi0[2], iz, noz);
+        const float n0 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+        const float f0 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        x0 = __builtin_fmaf(N.lo1[0], ix, nox); x1 = __builtin_fmaf(N.hi1[0], ix, nox);
+        y0 = __builtin_fmaf(N.lo1[1], iy, noy); y1 = __builtin_fmaf(N.hi1[1], iy, noy);
+        z0 = __builtin_fmaf(N.lo1[2], iz, noz); z1 = __builtin_fmaf(N.hi1[2], iz, noz);
+        const float n1 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+        const float f1 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        const bool h0 = !(n0 > f0), h1 = !(n1 > f1);
+        if (h0 && h1) {                                 // near child next, far child pushed
+            const bool swap = n1 < n0;
+            const uint32_t nearc = swap ? N.c1 : N.c0, farc = swap ? N.c0 : N.c1;
+            if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)farc; ++sp; }
+            else overflow = true;
+            cur = nearc;
+        } else if (h0 || h1) {
+            cur = h0 ? N.c0 : N.c1;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * STRIDE];
+        }
+    }
+    (void)overflow;  // unreachable: om_upload_world enables BVH2 only when depth <= DEPTH + 1
+    return best;
+}
+
+}  // namespace omd

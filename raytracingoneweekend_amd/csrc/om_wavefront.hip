@@ -43,8 +43,10 @@ void Buffers::release() {
 namespace {
 
 constexpr uint32_t kNoSample = 0xFFFFFFFFu;
-enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL = 5 };
+enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL = 5, TR_BVH2_LDS = 6, TR_BVH2_GLOBAL = 7 };
 constexpr int kBlk = 256;          // raygen / shade / intersect workgroup = one queue segment
+constexpr int kStackDepth = 24;                                   // BVH2 per-lane LDS stack (u16 entries)
+constexpr uint32_t kStackBytes = kBlk * kStackDepth * 2u;         // 12 KiB per 256-lane workgroup
 constexpr int kBlkLds = 1024;      // LDS-staged intersect workgroup = kSpbLds segments
 constexpr int kSpbLds = kBlkLds / kBlk;
 
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(kBlk) void k_raygen(OmCamDev C, OmParamsDev P, cons
 
 // ---------------------------------------------------------------- intersect
 // Workgroup b traces segments [b*SPB, b*SPB+SPB).
-template <int TR, int BLOCK, bool COUNT>
+template <int TR, int BLOCK, bool COUNT, bool MARCH>
 __global__ __launch_bounds__(BLOCK) void k_intersect(OmSceneDev S, OmParamsDev P, Seg G, const float4* __restrict__ q0,
                                                      const float4* __restrict__ q1, const uint32_t* __restrict__ count,
                                                      float2* __restrict__ hits, unsigned long long* __restrict__ counters) {
@@ -140,6 +142,18 @@ __global__ __launch_bounds__(BLOCK) void k_intersect(OmSceneDev S, OmParamsDev P
     uint32_t work = 0;
     for (uint32_t k = 0; k < SPB && s0 + k < G.nseg; ++k) work += count[s0 + k];
     if (work == 0) return;
+    if (TR == TR_BVH2_LDS) {                                      // [stack][nodes][leaf table]
+        const uint32_t nn = S.n_b2nodes * 4u;
+        const uint4* sn = (const uint4*)S.b2nodes;
+        uint4* dst = wf_lds + kStackBytes / 16u;
+        for (uint32_t i = threadIdx.x; i < nn; i += BLOCK) dst[i] = sn[i];
+        uint32_t* ldst = (uint32_t*)(dst + nn);
+        for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += BLOCK) ldst[i] = S.b2leaves[i];
+        __syncthreads();
+    }
+    uint16_t* stk = (uint16_t*)wf_lds + threadIdx.x;
+    const OmBvh2Node* b2_lds = (const OmBvh2Node*)(wf_lds + kStackBytes / 16u);
+    const uint32_t* b2_leaves_lds = (const uint32_t*)(wf_lds + kStackBytes / 16u + S.n_b2nodes * 4u);
     if (TR == TR_SBVH_LDS) {
         const uint32_t nn = S.n_snodes * 2u, nr = S.n_srecs * 4u;
         const uint4* sn = (const uint4*)S.snodes;
@@ -150,7 +164,8 @@ __global__ __launch_bounds__(BLOCK) void k_intersect(OmSceneDev S, OmParamsDev P
     }
     const OmSkipNode* lds_nodes = (const OmSkipNode*)wf_lds;
     const OmAffineTest* lds_recs = (const OmAffineTest*)(wf_lds + S.n_snodes * 2u);
-    const bool has_marched = (S.n_msph + S.n_mbox + S.n_mtor) != 0u;
+    // MARCH is a compile-time split: the sphere-tracing code (3 SDFs + unstuck) would
+    // otherwise set the register budget of every traced-only scene.
     WorkT<COUNT> w;
     for (uint32_t k = 0; k < SPB && s0 + k < G.nseg; ++k) {
         const uint32_t n = count[s0 + k];
@@ -161,11 +176,14 @@ __global__ __launch_bounds__(BLOCK) void k_intersect(OmSceneDev S, OmParamsDev P
             const F3 o = f3(a.x, a.y, a.z), d = f3(b.x, b.y, b.z);
             float closest = P.tmax;
             int best;
-            if (TR == TR_SBVH_LDS) best = traced_sbvh(S, lds_nodes, lds_recs, o, d, P.tmin, closest, w);
+            if (TR == TR_BVH2_LDS) best = traced_bvh2<kStackDepth, BLOCK>(S, b2_lds, b2_leaves_lds, stk, o, d, P.tmin, closest, w);
+            else if (TR == TR_BVH2_GLOBAL)
+                best = traced_bvh2<kStackDepth, BLOCK>(S, S.b2nodes, S.b2leaves, stk, o, d, P.tmin, closest, w);
+            else if (TR == TR_SBVH_LDS) best = traced_sbvh(S, lds_nodes, lds_recs, o, d, P.tmin, closest, w);
             else if (TR == TR_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
             else if (TR == TR_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
             else best = traced_brute<TR == TR_CULLED>(S, o, d, P.tmin, closest, w);
-            if (has_marched) {
+            if (MARCH) {
                 float tm;
                 const int mg = march(S, o, d, P.tmin, P.tmax, closest, P.march_steps, tm, w);
                 if (mg >= 0) { best = mg; closest = tm; }
@@ -333,10 +351,15 @@ void launch_intersect(bool count, uint32_t lds, hipStream_t st, const Launch& L,
                       const float4* q1, const uint32_t* cnt, float2* hits) {
     constexpr uint32_t SPB = BLOCK / kBlk;
     const uint32_t grid = (G.nseg + SPB - 1) / SPB;
-    if (count)
-        hipLaunchKernelGGL((k_intersect<TR, BLOCK, true>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
+    const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
+    if (count && march)
+        hipLaunchKernelGGL((k_intersect<TR, BLOCK, true, true>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
+    else if (count)
+        hipLaunchKernelGGL((k_intersect<TR, BLOCK, true, false>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
+    else if (march)
+        hipLaunchKernelGGL((k_intersect<TR, BLOCK, false, true>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
     else
-        hipLaunchKernelGGL((k_intersect<TR, BLOCK, false>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
+        hipLaunchKernelGGL((k_intersect<TR, BLOCK, false, false>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
 }
 
 }  // namespace
@@ -359,7 +382,8 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg);
     if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
     const bool lds_path = L.trace_mode == TR_SBVH_LDS && L.S.lds_bytes;
-    const int tr = (L.trace_mode == TR_SBVH_LDS && !L.S.lds_bytes) ? TR_SBVH_GLOBAL : L.trace_mode;
+    int tr = (L.trace_mode == TR_SBVH_LDS && !L.S.lds_bytes) ? TR_SBVH_GLOBAL : L.trace_mode;
+    if (tr == TR_BVH2_LDS) tr = L.S.n_b2nodes == 0 ? TR_BVH : (L.S.b2_lds_bytes ? TR_BVH2_LDS : TR_BVH2_GLOBAL);
     for (uint32_t done = 0; done < L.P.sample_count;) {
         const uint32_t b = std::min(batch, L.P.sample_count - done);
         const uint64_t paths = (uint64_t)n_px * b;
@@ -375,6 +399,10 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
             else if (tr == TR_BRUTE) launch_intersect<TR_BRUTE, kBlk>(L.count, 0, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
             else if (tr == TR_CULLED) launch_intersect<TR_CULLED, kBlk>(L.count, 0, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
             else if (tr == TR_BVH) launch_intersect<TR_BVH, kBlk>(L.count, 0, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
+            else if (tr == TR_BVH2_LDS)
+                launch_intersect<TR_BVH2_LDS, kBlk>(L.count, kStackBytes + L.S.b2_lds_bytes, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
+            else if (tr == TR_BVH2_GLOBAL)
+                launch_intersect<TR_BVH2_GLOBAL, kBlk>(L.count, kStackBytes, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
             else launch_intersect<TR_SBVH_GLOBAL, kBlk>(L.count, 0, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
             const int nx = 1 - cur;
             uint32_t* cnt_out = B.counts + (size_t)(bounce + 1) * nseg;

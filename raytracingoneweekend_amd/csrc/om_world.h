@@ -39,6 +39,9 @@ struct FrozenWorld {
     std::vector<OmSkipNode> snodes;    // stackless BVH (affine prims only)
     std::vector<OmAffineTest> srecs;   // its records in leaf order
     std::vector<uint32_t> always2;     // prims outside the stackless BVH
+    std::vector<OmBvh2Node> b2nodes;   // compressed BVH2 (same leaves/records as snodes)
+    std::vector<uint32_t> b2leaves;    // its leaf table: (first_record << 8) | count
+    uint32_t b2_depth = 0;             // its depth (stack bound)
     uint32_t counts[8];
     uint32_t offsets[9];               // global index offset per kind, offsets[8] = total
 };
