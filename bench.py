@@ -77,6 +77,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
     ap.add_argument("--pipeline", default="wavefront", choices=list(L.PIPELINES))
+    ap.add_argument("--tail", type=int, default=0, help="first bounce of the persistent tail launch (0 = library default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -100,6 +101,7 @@ def main():
     cam = om.default_camera(W / H)
     frozen = world.freeze(cam, device=local_rank, kernel=args.kernel, pipeline=args.pipeline)
     ctx = frozen.ctx
+    L.check(L.lib.om_set_tail_bounce(ctx, args.tail), ctx)
     spp_step = SPP_PER_STEP * world_size                     # fixed per-GPU samples per step
     spp_total = spp_step * args.steps
     pix = shard.tile_pixels(W, H, rank, world_size)
@@ -199,7 +201,8 @@ def main():
             "data": "synthetic: S-traced random_scene (om-rng seed 0x5EED), render seed 1",
             "config": {"workload": f"C1 S-traced {W}x{H}, {spp_total} spp timed ({spp_step} spp/step), depth {MAX_DEPTH}",
                        "width": W, "height": H, "spp_per_step": spp_step, "max_depth": MAX_DEPTH,
-                       "parallelism": f"tile{world_size}", "kernel": args.kernel, "pipeline": args.pipeline},
+                       "parallelism": f"tile{world_size}", "kernel": args.kernel, "pipeline": args.pipeline,
+                       "tail_bounce": args.tail or "default"},
             "hbm_gbs": round(hbm_gbs, 2),
             "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": None,

@@ -200,11 +200,16 @@ om_status om_reset_counters(om_ctx* ctx, void* stream);
  * compiled out (fewer registers); results are bit-identical either way. */
 om_status om_set_counting(om_ctx* ctx, int32_t enable);
 /* Execution pipeline (both bit-identical):
- *   OM_PIPELINE_WAVEFRONT  (default) raygen -> {intersect -> shade+compact} per bounce -> accumulate,
- *                          SoA ray queues in HBM
+ *   OM_PIPELINE_WAVEFRONT  (default) per bounce one {trace -> shade -> compact} launch over SoA
+ *                          path queues in HBM (bounce 0 generates the camera rays), then one
+ *                          persistent tail launch, then accumulate
  *   OM_PIPELINE_MEGAKERNEL one persistent-path kernel per call */
 enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1 };
 om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
+/* Wavefront pipeline: bounces >= `bounce` are finished by one persistent tail launch
+ * (lanes run whole remaining paths); 0 = default (16), >= max_depth = no tail.  A pure
+ * scheduling knob: results are bit-identical for every value. */
+om_status om_set_tail_bounce(om_ctx* ctx, uint32_t bounce);
 
 #ifdef __cplusplus
 }

@@ -61,6 +61,7 @@ EXPORTS = [
     "om_world_random_scene", "om_world_basic_scene", "om_world_marched_scene", "om_create", "om_destroy",
     "om_last_error", "om_upload_world", "om_set_kernel", "om_render", "om_render_device",
     "om_render_device_pixels", "om_get_counters", "om_reset_counters", "om_set_counting", "om_set_pipeline",
+    "om_set_tail_bounce",
 ]
 
 
@@ -135,6 +136,7 @@ def _load():
         "om_reset_counters": (st, [vp, vp]),
         "om_set_counting": (st, [vp, C.c_int32]),
         "om_set_pipeline": (st, [vp, C.c_int32]),
+        "om_set_tail_bounce": (st, [vp, C.c_uint32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

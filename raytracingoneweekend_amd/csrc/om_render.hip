@@ -243,6 +243,7 @@ struct om_ctx {
     hipStream_t last_stream = nullptr;
     bool count_work = true;
     int pipeline = OM_PIPELINE_WAVEFRONT;
+    uint32_t tail_bounce = 0;
     omw::Buffers wf;
     DevBuf frame_list;                  // tile-ordered pixel list of the full frame (wavefront path)
     uint32_t frame_w = 0, frame_h = 0;
@@ -380,6 +381,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         L.stats = dev_stats;
         L.counters = (unsigned long long*)c->counters.p;
         L.count = c->count_work;
+        L.tail_bounce = c->tail_bounce;
         L.trace_mode = mode == OM_KERNEL_BRUTE ? MODE_BRUTE : mode == OM_KERNEL_CULLED ? MODE_CULLED
                      : mode == OM_KERNEL_BVH ? MODE_BVH : mode == OM_KERNEL_BVH2 ? 6 : MODE_SBVH_LDS;
         if (dev_pixels) {
@@ -568,6 +570,12 @@ om_status om_set_pipeline(om_ctx* c, int32_t pipeline) {
     if (pipeline != OM_PIPELINE_MEGAKERNEL && pipeline != OM_PIPELINE_WAVEFRONT)
         return set_err(c, OM_ERR_INVALID, "om_set_pipeline: unknown pipeline");
     c->pipeline = pipeline;
+    return OM_OK;
+}
+
+om_status om_set_tail_bounce(om_ctx* c, uint32_t bounce) {
+    if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
+    c->tail_bounce = bounce;
     return OM_OK;
 }
 

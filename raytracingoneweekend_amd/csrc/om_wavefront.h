@@ -15,7 +15,6 @@ struct Buffers {
     uint64_t cap = 0;            // paths per batch
     float4* q[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};  // ping-pong queues: o|depthf, d|first_id, cur|seg
     uint4* qr[2] = {nullptr, nullptr};   // rng lo, rng hi, path slot, pad
-    float2* hits = nullptr;      // t, gi (bits)
     float4* res = nullptr;       // colour.xyz, depth
     uint32_t* res_id = nullptr;  // obj id (0xFFFFFFFF = no sample)
     uint32_t* counts = nullptr;  // per bounce, per queue segment: live rays
@@ -35,6 +34,7 @@ struct Launch {
     unsigned long long* counters;
     bool count;
     int trace_mode;              // closest-hit kernel variant (om_render.hip MODE_*)
+    uint32_t tail_bounce;        // first bounce run by the persistent tail kernel (0 = default)
 };
 
 // Renders P.sample_count samples of every listed pixel; returns 0 or a HIP error text.

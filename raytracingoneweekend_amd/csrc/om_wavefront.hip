@@ -1,12 +1,16 @@
 // om_wavefront.hip — wavefront path tracer: the bounce recursion of
-// ray_color (render_thread.rs:128-143) flattened into per-bounce kernels over SoA ray
-// queues in HBM:
+// ray_color (render_thread.rs:128-143) flattened into per-bounce launches over SoA
+// path queues in HBM:
 //
-//   raygen      one lane per (sample, pixel): camera ray (render_thread.rs:183-192)
-//   intersect   one lane per live ray: closest hit (hits.rs:270-365) -> (t, gi)
-//   shade       one lane per live ray: HitRecord + Material::scatter / sky
-//               (render_thread.rs:105-126); survivors are compacted into the next
-//               queue, finished paths write (colour, depth, id) to their result slot
+//   bounce 0    one lane per (sample, pixel): camera ray (render_thread.rs:183-192),
+//               closest hit (hits.rs:270-365), HitRecord + Material::scatter / sky
+//               (render_thread.rs:105-126); survivors are compacted into queue 1,
+//               finished paths write (colour, depth, id) to their result slot
+//   bounce b    the same from queue b: trace + shade + compaction in ONE kernel (the
+//               path state is read once and written once per bounce; no hit buffer)
+//   tail        from bounce T on the queues hold a few thousand paths: one persistent
+//               launch runs every remaining path to completion, lanes stealing paths
+//               from a per-workgroup LDS counter (no ~40 near-empty launch pairs)
 //   accumulate  one lane per pixel: Stats::add over the batch's samples IN SAMPLE
 //               ORDER (render_thread.rs:23-39): bit-identical to the sequential
 //               reference and to the megakernel.
@@ -33,22 +37,21 @@ void Buffers::release() {
         for (int b = 0; b < 3; ++b) { if (q[a][b]) (void)hipFree(q[a][b]); q[a][b] = nullptr; }
         if (qr[a]) (void)hipFree(qr[a]); qr[a] = nullptr;
     }
-    if (hits) (void)hipFree(hits);
     if (res) (void)hipFree(res);
     if (res_id) (void)hipFree(res_id);
     if (counts) (void)hipFree(counts);
-    hits = nullptr; res = nullptr; res_id = nullptr; counts = nullptr; cap = 0; counts_n = 0;
+    res = nullptr; res_id = nullptr; counts = nullptr; cap = 0; counts_n = 0;
 }
 
 namespace {
 
 constexpr uint32_t kNoSample = 0xFFFFFFFFu;
 enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL = 5, TR_BVH2_LDS = 6, TR_BVH2_GLOBAL = 7 };
-constexpr int kBlk = 256;          // raygen / shade / intersect workgroup = one queue segment
+constexpr int kBlk = 256;                                         // workgroup = one queue segment
 constexpr int kStackDepth = 24;                                   // BVH2 per-lane LDS stack (u16 entries)
 constexpr uint32_t kStackBytes = kBlk * kStackDepth * 2u;         // 12 KiB per 256-lane workgroup
-constexpr int kBlkLds = 1024;      // LDS-staged intersect workgroup = kSpbLds segments
-constexpr int kSpbLds = kBlkLds / kBlk;
+constexpr uint32_t kTailSpb = 4;                                  // queue segments per tail workgroup
+constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
 
 extern __shared__ __attribute__((aligned(16))) uint4 wf_lds[];
 
@@ -84,199 +87,253 @@ __device__ __forceinline__ void flush_counter(unsigned long long* ctr, int slot,
 }
 
 struct Seg {
-    uint32_t nseg;    // segments (= shade/raygen workgroups)
-    uint32_t segcap;  // rays per segment
+    uint32_t nseg;    // segments (= bounce workgroups)
+    uint32_t segcap;  // paths per segment
 };
 
-// ---------------------------------------------------------------- raygen
-__global__ __launch_bounds__(kBlk) void k_raygen(OmCamDev C, OmParamsDev P, const float2* __restrict__ jitter,
-                                                 const om_pixel_stats* __restrict__ stats, const uint32_t* __restrict__ pixels,
-                                                 uint32_t n_pixels, uint32_t by_pixel, uint32_t batch, Seg G,
-                                                 float4* __restrict__ q0, float4* __restrict__ q1, float4* __restrict__ q2,
-                                                 uint4* __restrict__ qr, uint32_t* __restrict__ count,
-                                                 uint32_t* __restrict__ res_id) {
-    const uint64_t paths = (uint64_t)n_pixels * batch;
-    const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
-    const uint64_t end = std::min<uint64_t>(seg0 + G.segcap, paths);
-    uint32_t run = 0;
-    for (uint64_t base = seg0; base < end; base += kBlk) {
-        const uint64_t t = base + threadIdx.x;
-        bool ok = false;
-        F3 o = f3(0, 0, 0), d = f3(0, 0, 0);
-        Rng g; g.s = 0;
-        if (t < end) {
-            const uint32_t s_local = (uint32_t)(t / n_pixels), k = (uint32_t)(t - (uint64_t)s_local * n_pixels);
-            const uint32_t pixel = pixels[k];
-            const uint32_t slot = by_pixel ? pixel : k;
-            const uint32_t s = stats[slot].n + s_local;
-            ok = s < P.spp_total && !(P.adaptive && (stats[slot].flags & 1u));
-            res_id[t] = kNoSample;
-            if (ok) {
-                g = path_rng(P.skey, pixel, s);
-                const uint32_t line = pixel / P.width;
-                gen_camera_ray(C, P, jitter, (float)(pixel - P.width * line), (float)line, s, g, o, d);
-            }
-        }
-        uint32_t tot;
-        const uint32_t j = block_scan(ok, tot);
-        if (ok) {
-            const uint64_t at_ = seg0 + run + j;
-            q0[at_] = make_float4(o.x, o.y, o.z, 0.0f);
-            q1[at_] = make_float4(d.x, d.y, d.z, __uint_as_float(0u));
-            q2[at_] = make_float4(1.0f, 1.0f, 1.0f, __uint_as_float(0u));
-            qr[at_] = make_uint4((uint32_t)g.s, (uint32_t)(g.s >> 32), (uint32_t)t, 0u);
-        }
-        run += tot;
-    }
-    if (threadIdx.x == 0) count[blockIdx.x] = run;
+// One SoA path queue: o|depthf, d|first_id, throughput|segment, rng lo|rng hi|slot|-.
+struct Queue {
+    float4* q0; float4* q1; float4* q2; uint4* qr;
+};
+
+// Primary-ray source of bounce 0 (render_thread.rs:176-192).
+struct Gen {
+    OmCamDev C;
+    const float2* jitter;
+    const om_pixel_stats* stats;
+    const uint32_t* pixels;      // tile-ordered pixel list
+    uint32_t n_pixels, by_pixel, batch;
+};
+
+// A path between bounces: ray_color's loop state (render_thread.rs:128-143).
+struct Path {
+    F3 o, d, cur;
+    float depthf;
+    uint32_t first_id, seg, slot;
+    Rng g;
+};
+
+__device__ __forceinline__ void load_ray(const Queue& Q, uint64_t i, Path& p) {
+    const float4 a = Q.q0[i], b = Q.q1[i];
+    p.o = f3(a.x, a.y, a.z); p.depthf = a.w;
+    p.d = f3(b.x, b.y, b.z); p.first_id = __float_as_uint(b.w);
+}
+__device__ __forceinline__ void load_rest(const Queue& Q, uint64_t i, Path& p) {
+    const float4 c = Q.q2[i];
+    const uint4 r = Q.qr[i];
+    p.cur = f3(c.x, c.y, c.z); p.seg = __float_as_uint(c.w);
+    p.g.s = ((uint64_t)r.y << 32) | r.x; p.slot = r.z;
+}
+__device__ __forceinline__ void store_path(const Queue& Q, uint64_t i, const Path& p) {
+    Q.q0[i] = make_float4(p.o.x, p.o.y, p.o.z, p.depthf);
+    Q.q1[i] = make_float4(p.d.x, p.d.y, p.d.z, __uint_as_float(p.first_id));
+    Q.q2[i] = make_float4(p.cur.x, p.cur.y, p.cur.z, __uint_as_float(p.seg));
+    Q.qr[i] = make_uint4((uint32_t)p.g.s, (uint32_t)(p.g.s >> 32), p.slot, 0u);
 }
 
-// ---------------------------------------------------------------- intersect
-// Workgroup b traces segments [b*SPB, b*SPB+SPB).
-template <int TR, int BLOCK, bool COUNT, bool MARCH>
-__global__ __launch_bounds__(BLOCK) void k_intersect(OmSceneDev S, OmParamsDev P, Seg G, const float4* __restrict__ q0,
-                                                     const float4* __restrict__ q1, const uint32_t* __restrict__ count,
-                                                     float2* __restrict__ hits, unsigned long long* __restrict__ counters) {
-    constexpr uint32_t SPB = BLOCK / kBlk;
-    const uint32_t s0 = blockIdx.x * SPB;
-    uint32_t work = 0;
-    for (uint32_t k = 0; k < SPB && s0 + k < G.nseg; ++k) work += count[s0 + k];
-    if (work == 0) return;
-    if (TR == TR_BVH2_LDS) {                                      // [stack][nodes][leaf table]
+// Scene data a workgroup traces against: BVH2 nodes + leaf table staged in LDS behind
+// the per-lane stack ([stack][nodes][leaf table]), or read through L2.
+struct Tracer {
+    const OmBvh2Node* b2n;
+    const uint32_t* b2l;
+    uint16_t* stk;
+};
+
+template <int TR>
+__device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every thread of the block calls it
+    Tracer t;
+    t.stk = (uint16_t*)wf_lds + threadIdx.x;
+    t.b2n = S.b2nodes; t.b2l = S.b2leaves;
+    if (TR == TR_BVH2_LDS) {
         const uint32_t nn = S.n_b2nodes * 4u;
         const uint4* sn = (const uint4*)S.b2nodes;
         uint4* dst = wf_lds + kStackBytes / 16u;
-        for (uint32_t i = threadIdx.x; i < nn; i += BLOCK) dst[i] = sn[i];
+        for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = sn[i];
         uint32_t* ldst = (uint32_t*)(dst + nn);
-        for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += BLOCK) ldst[i] = S.b2leaves[i];
+        for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += kBlk) ldst[i] = S.b2leaves[i];
         __syncthreads();
+        t.b2n = (const OmBvh2Node*)dst; t.b2l = ldst;
     }
-    uint16_t* stk = (uint16_t*)wf_lds + threadIdx.x;
-    const OmBvh2Node* b2_lds = (const OmBvh2Node*)(wf_lds + kStackBytes / 16u);
-    const uint32_t* b2_leaves_lds = (const uint32_t*)(wf_lds + kStackBytes / 16u + S.n_b2nodes * 4u);
-    if (TR == TR_SBVH_LDS) {
-        const uint32_t nn = S.n_snodes * 2u, nr = S.n_srecs * 4u;
-        const uint4* sn = (const uint4*)S.snodes;
-        const uint4* sr = (const uint4*)S.srecs;
-        for (uint32_t i = threadIdx.x; i < nn; i += BLOCK) wf_lds[i] = sn[i];
-        for (uint32_t i = threadIdx.x; i < nr; i += BLOCK) wf_lds[nn + i] = sr[i];
-        __syncthreads();
+    return t;
+}
+
+// Closest hit of one ray (hits.rs:270-365): -> (closest, global prim index or -1).
+// MARCH is a compile-time split: the sphere-tracing code (3 SDFs + unstuck) would
+// otherwise set the register budget of every traced-only scene.
+template <int TR, bool MARCH, class Wk>
+__device__ __forceinline__ int trace(const OmSceneDev& S, const OmParamsDev& P, const Tracer& T, F3 o, F3 d,
+                                     float& closest, Wk& w) {
+    closest = P.tmax;
+    int best;
+    if (TR == TR_BVH2_LDS || TR == TR_BVH2_GLOBAL) best = traced_bvh2<kStackDepth, kBlk>(S, T.b2n, T.b2l, T.stk, o, d, P.tmin, closest, w);
+    else if (TR == TR_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
+    else if (TR == TR_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
+    else best = traced_brute<TR == TR_CULLED>(S, o, d, P.tmin, closest, w);
+    if (MARCH) {
+        float tm;
+        const int mg = march(S, o, d, P.tmin, P.tmax, closest, P.march_steps, tm, w);
+        if (mg >= 0) { best = mg; closest = tm; }
     }
-    const OmSkipNode* lds_nodes = (const OmSkipNode*)wf_lds;
-    const OmAffineTest* lds_recs = (const OmAffineTest*)(wf_lds + S.n_snodes * 2u);
-    // MARCH is a compile-time split: the sphere-tracing code (3 SDFs + unstuck) would
-    // otherwise set the register budget of every traced-only scene.
+    return best;
+}
+
+// handle_hit + ray_color's termination rules (render_thread.rs:105-143) for one
+// segment.  Returns true when the path continues (p advanced to the next segment);
+// otherwise the sample's (colour, depth, id) is written to its result slot.
+__device__ __forceinline__ bool shade_path(const OmSceneDev& S, const OmParamsDev& P, uint32_t depth_cap, Path& p,
+                                           float closest, int best, float4* __restrict__ res,
+                                           uint32_t* __restrict__ res_id) {
+    float seg_depth; uint32_t seg_id;
+    if (best >= 0) {                                                   // handle_hit, Some(hr)
+        F3 point, normal;
+        finalize(S, best, p.o, p.d, P.tmin, closest, point, normal);
+        F3 nd, att;
+        scatter(S.mats[best], p.d, normal, p.g, nd, att);
+        p.cur = mul(p.cur, att);
+        p.o = point; p.d = unit(nd);
+        seg_depth = closest; seg_id = (uint32_t)best + 1u;
+    } else {                                                           // None: sky (render_thread.rs:118-120)
+        const float t = 0.5f * (p.d.y + 1.0f);
+        p.cur = mul(p.cur, f3((1.0f - t) + 0.5f * t, (1.0f - t) + 0.7f * t, (1.0f - t) + 1.0f * t));
+        seg_depth = INFINITY; seg_id = 0u;
+    }
+    bool finished = false;
+    F3 result = p.cur;
+    float rdepth = 0.0f; uint32_t rid = 0;
+    if (p.seg == 0u) {
+        p.depthf = seg_depth; p.first_id = seg_id;
+        if (isinf(seg_depth)) { finished = true; rdepth = INFINITY; rid = 0u; }         // :133-135
+    } else if (isinf(seg_depth)) {
+        finished = true; rdepth = p.depthf; rid = p.first_id;                            // :138-140
+    }
+    if (!finished && p.seg + 1u >= depth_cap) {                                          // :142 -Color::ZERO
+        finished = true; result = f3(-0.0f, -0.0f, -0.0f); rdepth = p.depthf; rid = p.first_id;
+    }
+    if (finished) {
+        res[p.slot] = make_float4(result.x, result.y, result.z, rdepth);
+        res_id[p.slot] = rid;
+        return false;
+    }
+    p.seg += 1u;
+    return true;
+}
+
+// ---------------------------------------------------------------- bounce
+// Workgroup s: the paths of segment s of queue `in` (FIRST: the camera samples
+// [s*segcap, (s+1)*segcap) of the batch) -> survivors into segment s of `out`.
+template <int TR, bool COUNT, bool MARCH, bool FIRST>
+__global__ __launch_bounds__(kBlk) void k_bounce(OmSceneDev S, OmParamsDev P, Seg G, Gen R, Queue in,
+                                                 const uint32_t* __restrict__ count_in, Queue out,
+                                                 uint32_t* __restrict__ count_out, float4* __restrict__ res,
+                                                 uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters) {
+    const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
+    uint32_t n;
+    if (FIRST) {
+        const uint64_t paths = (uint64_t)R.n_pixels * R.batch;
+        n = seg0 < paths ? (uint32_t)std::min<uint64_t>(G.segcap, paths - seg0) : 0u;
+    } else {
+        n = count_in[blockIdx.x];
+    }
+    if (n == 0) {
+        if (threadIdx.x == 0) count_out[blockIdx.x] = 0u;
+        return;
+    }
+    const Tracer T = stage_scene<TR>(S);
+    const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
     WorkT<COUNT> w;
-    for (uint32_t k = 0; k < SPB && s0 + k < G.nseg; ++k) {
-        const uint32_t n = count[s0 + k];
-        const uint64_t seg0 = (uint64_t)(s0 + k) * G.segcap;
-        for (uint32_t j = threadIdx.x; j < n; j += BLOCK) {
-            const uint64_t i = seg0 + j;
-            const float4 a = q0[i], b = q1[i];
-            const F3 o = f3(a.x, a.y, a.z), d = f3(b.x, b.y, b.z);
-            float closest = P.tmax;
-            int best;
-            if (TR == TR_BVH2_LDS) best = traced_bvh2<kStackDepth, BLOCK>(S, b2_lds, b2_leaves_lds, stk, o, d, P.tmin, closest, w);
-            else if (TR == TR_BVH2_GLOBAL)
-                best = traced_bvh2<kStackDepth, BLOCK>(S, S.b2nodes, S.b2leaves, stk, o, d, P.tmin, closest, w);
-            else if (TR == TR_SBVH_LDS) best = traced_sbvh(S, lds_nodes, lds_recs, o, d, P.tmin, closest, w);
-            else if (TR == TR_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
-            else if (TR == TR_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
-            else best = traced_brute<TR == TR_CULLED>(S, o, d, P.tmin, closest, w);
-            if (MARCH) {
-                float tm;
-                const int mg = march(S, o, d, P.tmin, P.tmax, closest, P.march_steps, tm, w);
-                if (mg >= 0) { best = mg; closest = tm; }
+    uint32_t segs = 0, run = 0;
+    for (uint32_t base = 0; base < n; base += kBlk) {
+        const uint32_t jj = base + threadIdx.x;
+        bool keep = false;
+        Path p;
+        if (jj < n) {
+            const uint64_t i = seg0 + jj;
+            bool live = true;
+            if (FIRST) {
+                const uint32_t s_local = (uint32_t)(i / R.n_pixels), k = (uint32_t)(i - (uint64_t)s_local * R.n_pixels);
+                const uint32_t pixel = R.pixels[k];
+                const om_pixel_stats& ps = R.stats[R.by_pixel ? pixel : k];
+                const uint32_t s = ps.n + s_local;
+                live = s < P.spp_total && !(P.adaptive && (ps.flags & 1u));
+                if (live) {
+                    p.g = path_rng(P.skey, pixel, s);
+                    const uint32_t line = pixel / P.width;
+                    gen_camera_ray(R.C, P, R.jitter, (float)(pixel - P.width * line), (float)line, s, p.g, p.o, p.d);
+                    p.cur = f3(1.0f, 1.0f, 1.0f); p.depthf = 0.0f; p.first_id = 0u; p.seg = 0u; p.slot = (uint32_t)i;
+                } else {
+                    res_id[i] = kNoSample;
+                }
+            } else {
+                load_ray(in, i, p);
             }
-            hits[i] = make_float2(closest, __int_as_float(best));
+            if (live) {
+                float closest;
+                const int best = trace<TR, MARCH>(S, P, T, p.o, p.d, closest, w);
+                if (!FIRST) load_rest(in, i, p);
+                keep = shade_path(S, P, depth_cap, p, closest, best, res, res_id);
+                if (COUNT) segs++;
+            }
         }
+        uint32_t tot;
+        const uint32_t j = block_scan(keep, tot);
+        if (keep) store_path(out, seg0 + run + j, p);
+        run += tot;
     }
+    if (threadIdx.x == 0) count_out[blockIdx.x] = run;
     if (COUNT) {
+        flush_counter(counters, OMC_SEGMENTS, segs);
         flush_counter(counters, OMC_PRIM_TESTS, w.prim);
         flush_counter(counters, OMC_PRE_TESTS, w.pre);
         flush_counter(counters, OMC_MARCH, w.march);
     }
 }
 
-// ---------------------------------------------------------------- shade
-template <bool COUNT>
-__global__ __launch_bounds__(kBlk) void k_shade(OmSceneDev S, OmParamsDev P, Seg G,
-                                                const float4* __restrict__ i0, const float4* __restrict__ i1,
-                                                const float4* __restrict__ i2, const uint4* __restrict__ ir,
-                                                const uint32_t* __restrict__ count_in, const float2* __restrict__ hits,
-                                                float4* __restrict__ o0, float4* __restrict__ o1, float4* __restrict__ o2,
-                                                uint4* __restrict__ orr, uint32_t* __restrict__ count_out,
-                                                float4* __restrict__ res, uint32_t* __restrict__ res_id,
-                                                unsigned long long* __restrict__ counters) {
-    const uint32_t n = count_in[blockIdx.x];
-    const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
-    const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
-    uint32_t segs = 0, run = 0;
-    for (uint32_t base = 0; base < n; base += kBlk) {
-        const uint32_t jj = base + threadIdx.x;
-        const bool valid = jj < n;
-        const uint64_t i = seg0 + jj;
-        bool keep = false;
-        float4 a = make_float4(0, 0, 0, 0), b = a, c = a;
-        uint4 r = make_uint4(0, 0, 0, 0);
-        if (valid) {
-            a = i0[i]; b = i1[i]; c = i2[i]; r = ir[i];
-            const float2 h = hits[i];
-            const int best = __float_as_int(h.y);
-            const float closest = h.x;
-            F3 o = f3(a.x, a.y, a.z), d = f3(b.x, b.y, b.z), cur = f3(c.x, c.y, c.z);
-            float depthf = a.w;
-            uint32_t first_id = __float_as_uint(b.w);
-            const uint32_t seg = __float_as_uint(c.w);
-            Rng g; g.s = ((uint64_t)r.y << 32) | r.x;
-            float seg_depth; uint32_t seg_id;
-            if (best >= 0) {                                                   // handle_hit, Some(hr)
-                F3 point, normal;
-                finalize(S, best, o, d, P.tmin, closest, point, normal);
-                F3 nd, att;
-                scatter(S.mats[best], d, normal, g, nd, att);
-                cur = mul(cur, att);
-                o = point; d = unit(nd);
-                seg_depth = closest; seg_id = (uint32_t)best + 1u;
-            } else {                                                           // None: sky (render_thread.rs:118-120)
-                const float t = 0.5f * (d.y + 1.0f);
-                cur = mul(cur, f3((1.0f - t) + 0.5f * t, (1.0f - t) + 0.7f * t, (1.0f - t) + 1.0f * t));
-                seg_depth = INFINITY; seg_id = 0u;
-            }
-            bool finished = false;
-            F3 result = cur;
-            float rdepth = 0.0f; uint32_t rid = 0;
-            if (seg == 0u) {
-                depthf = seg_depth; first_id = seg_id;
-                if (isinf(seg_depth)) { finished = true; rdepth = INFINITY; rid = 0u; }       // :133-135
-            } else if (isinf(seg_depth)) {
-                finished = true; rdepth = depthf; rid = first_id;                         // :138-140
-            }
-            if (!finished && seg + 1u >= depth_cap) {                                        // :142 -Color::ZERO
-                finished = true; result = f3(-0.0f, -0.0f, -0.0f); rdepth = depthf; rid = first_id;
-            }
-            if (finished) {
-                res[r.z] = make_float4(result.x, result.y, result.z, rdepth);
-                res_id[r.z] = rid;
-            } else {
-                keep = true;
-                a = make_float4(o.x, o.y, o.z, depthf);
-                b = make_float4(d.x, d.y, d.z, __uint_as_float(first_id));
-                c = make_float4(cur.x, cur.y, cur.z, __uint_as_float(seg + 1u));
-                r = make_uint4((uint32_t)g.s, (uint32_t)(g.s >> 32), r.z, 0u);
-            }
-            if (COUNT) segs++;
+// ---------------------------------------------------------------- tail
+// Workgroup b: every path of segments [b*kTailSpb, (b+1)*kTailSpb) of queue `in`, each
+// run to completion; a lane whose path ends takes the next one from an LDS counter.
+template <int TR, bool COUNT, bool MARCH>
+__global__ __launch_bounds__(kBlk) void k_tail(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
+                                               const uint32_t* __restrict__ count_in, float4* __restrict__ res,
+                                               uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters) {
+    __shared__ uint32_t pre[kTailSpb + 1];
+    __shared__ uint32_t next;
+    const uint32_t s0 = blockIdx.x * kTailSpb;
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < kTailSpb; ++k) {
+            pre[k] = acc;
+            acc += s0 + k < G.nseg ? count_in[s0 + k] : 0u;
         }
-        uint32_t tot;
-        const uint32_t j = block_scan(keep, tot);
-        if (keep) {
-            const uint64_t at_ = seg0 + run + j;
-            o0[at_] = a; o1[at_] = b; o2[at_] = c; orr[at_] = r;
-        }
-        run += tot;
+        pre[kTailSpb] = acc;
+        next = kBlk;
     }
-    if (threadIdx.x == 0) count_out[blockIdx.x] = run;
-    if (COUNT) flush_counter(counters, OMC_SEGMENTS, segs);
+    __syncthreads();
+    const uint32_t total = pre[kTailSpb];
+    if (total == 0) return;
+    const Tracer T = stage_scene<TR>(S);
+    const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
+    WorkT<COUNT> w;
+    uint32_t segs = 0;
+    for (uint32_t idx = threadIdx.x; idx < total; idx = atomicAdd(&next, 1u)) {
+        uint32_t k = 0;
+        while (idx >= pre[k + 1]) ++k;
+        const uint64_t i = (uint64_t)(s0 + k) * G.segcap + (idx - pre[k]);
+        Path p;
+        load_ray(in, i, p);
+        load_rest(in, i, p);
+        for (;;) {
+            float closest;
+            const int best = trace<TR, MARCH>(S, P, T, p.o, p.d, closest, w);
+            if (COUNT) segs++;
+            if (!shade_path(S, P, depth_cap, p, closest, best, res, res_id)) break;
+        }
+    }
+    if (COUNT) {
+        flush_counter(counters, OMC_SEGMENTS, segs);
+        flush_counter(counters, OMC_PRIM_TESTS, w.prim);
+        flush_counter(counters, OMC_PRE_TESTS, w.pre);
+        flush_counter(counters, OMC_MARCH, w.march);
+    }
 }
 
 // ---------------------------------------------------------------- accumulate
@@ -331,7 +388,6 @@ hipError_t grow(Buffers& B, uint64_t cap, uint32_t counts_n) {
             for (int b = 0; b < 3; ++b) if ((e = hipMalloc(&B.q[a][b], cap * sizeof(float4))) != hipSuccess) return e;
             if ((e = hipMalloc(&B.qr[a], cap * sizeof(uint4))) != hipSuccess) return e;
         }
-        if ((e = hipMalloc(&B.hits, cap * sizeof(float2))) != hipSuccess) return e;
         if ((e = hipMalloc(&B.res, cap * sizeof(float4))) != hipSuccess) return e;
         if ((e = hipMalloc(&B.res_id, cap * sizeof(uint32_t))) != hipSuccess) return e;
         B.cap = cap;
@@ -346,20 +402,38 @@ hipError_t grow(Buffers& B, uint64_t cap, uint32_t counts_n) {
     return hipSuccess;
 }
 
-template <int TR, int BLOCK>
-void launch_intersect(bool count, uint32_t lds, hipStream_t st, const Launch& L, Seg G, const float4* q0,
-                      const float4* q1, const uint32_t* cnt, float2* hits) {
-    constexpr uint32_t SPB = BLOCK / kBlk;
-    const uint32_t grid = (G.nseg + SPB - 1) / SPB;
-    const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
-    if (count && march)
-        hipLaunchKernelGGL((k_intersect<TR, BLOCK, true, true>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
-    else if (count)
-        hipLaunchKernelGGL((k_intersect<TR, BLOCK, true, false>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
-    else if (march)
-        hipLaunchKernelGGL((k_intersect<TR, BLOCK, false, true>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
-    else
-        hipLaunchKernelGGL((k_intersect<TR, BLOCK, false, false>), dim3(grid), dim3(BLOCK), lds, st, L.S, L.P, G, q0, q1, cnt, hits, L.counters);
+Queue queue(Buffers& B, int k) { return Queue{B.q[k][0], B.q[k][1], B.q[k][2], B.qr[k]}; }
+
+// One batch: bounce 0 .. tail_at-1 as per-bounce launches, then the tail launch.
+template <int TR, bool COUNT, bool MARCH>
+void run_batch(Buffers& B, const Launch& L, hipStream_t st, Seg G, const Gen& R, uint32_t depth_cap,
+               uint32_t tail_at, uint32_t lds) {
+    for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
+        const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
+        const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
+        if (bounce > 0 && bounce >= tail_at) {
+            const uint32_t grid = (G.nseg + kTailSpb - 1u) / kTailSpb;
+            hipLaunchKernelGGL((k_tail<TR, COUNT, MARCH>), dim3(grid), dim3(kBlk), lds, st, L.S, L.P, G, in, cin,
+                               B.res, B.res_id, L.counters);
+            return;
+        }
+        uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
+        if (bounce == 0)
+            hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, true>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
+                               cin, out, cout, B.res, B.res_id, L.counters);
+        else
+            hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
+                               cin, out, cout, B.res, B.res_id, L.counters);
+    }
+}
+
+template <int TR>
+void run_tr(bool count, bool march, Buffers& B, const Launch& L, hipStream_t st, Seg G, const Gen& R,
+            uint32_t depth_cap, uint32_t tail_at, uint32_t lds) {
+    if (count && march) run_batch<TR, true, true>(B, L, st, G, R, depth_cap, tail_at, lds);
+    else if (count) run_batch<TR, true, false>(B, L, st, G, R, depth_cap, tail_at, lds);
+    else if (march) run_batch<TR, false, true>(B, L, st, G, R, depth_cap, tail_at, lds);
+    else run_batch<TR, false, false>(B, L, st, G, R, depth_cap, tail_at, lds);
 }
 
 }  // namespace
@@ -367,54 +441,42 @@ void launch_intersect(bool count, uint32_t lds, hipStream_t st, const Launch& L,
 hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err) {
     const uint32_t n_px = L.n_pixels;
     if (n_px == 0 || L.P.sample_count == 0) return hipSuccess;
-    const uint64_t kMaxPaths = 1ull << 25;   // 33.5M paths per batch (~5.3 GB of queues)
+    const uint64_t kMaxPaths = 1ull << 25;   // 33.5M paths per batch (~4.9 GB of queues)
     const uint32_t batch = L.P.adaptive ? 1u : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));
     const uint32_t depth_cap = L.P.max_depth > 1u ? L.P.max_depth : 1u;
+    const uint32_t tail_at = L.tail_bounce ? L.tail_bounce : kTailDefault;
     int dev = 0;
     (void)hipGetDevice(&dev);
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint64_t max_paths = (uint64_t)n_px * batch;
-    // segments: a multiple of the LDS-intersect grouping, ~16 workgroups per CU
+    // segments: ~16 workgroups per CU, a multiple of the tail grouping
     uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * 16u);
-    nseg = (nseg + kSpbLds - 1) / kSpbLds * kSpbLds;
+    nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
     const uint32_t segcap = (uint32_t)((max_paths + nseg - 1) / nseg);
     hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg);
     if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
-    const bool lds_path = L.trace_mode == TR_SBVH_LDS && L.S.lds_bytes;
-    int tr = (L.trace_mode == TR_SBVH_LDS && !L.S.lds_bytes) ? TR_SBVH_GLOBAL : L.trace_mode;
+    int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
     if (tr == TR_BVH2_LDS) tr = L.S.n_b2nodes == 0 ? TR_BVH : (L.S.b2_lds_bytes ? TR_BVH2_LDS : TR_BVH2_GLOBAL);
+    const uint32_t lds = tr == TR_BVH2_LDS ? kStackBytes + L.S.b2_lds_bytes : tr == TR_BVH2_GLOBAL ? kStackBytes : 0u;
+    const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
+    Gen R;
+    R.C = L.C; R.jitter = L.jitter; R.stats = L.stats; R.pixels = L.pixels; R.n_pixels = n_px;
+    R.by_pixel = L.stats_by_pixel ? 1u : 0u;
     for (uint32_t done = 0; done < L.P.sample_count;) {
         const uint32_t b = std::min(batch, L.P.sample_count - done);
         const uint64_t paths = (uint64_t)n_px * b;
         Seg G;
         G.nseg = nseg;
         G.segcap = (uint32_t)((paths + nseg - 1) / nseg);
-        hipLaunchKernelGGL(k_raygen, dim3(nseg), dim3(kBlk), 0, st, L.C, L.P, L.jitter, L.stats, L.pixels, n_px,
-                           L.stats_by_pixel ? 1u : 0u, b, G, B.q[0][0], B.q[0][1], B.q[0][2], B.qr[0], B.counts, B.res_id);
-        int cur = 0;
-        for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
-            const uint32_t* cnt = B.counts + (size_t)bounce * nseg;
-            if (lds_path) launch_intersect<TR_SBVH_LDS, kBlkLds>(L.count, L.S.lds_bytes, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
-            else if (tr == TR_BRUTE) launch_intersect<TR_BRUTE, kBlk>(L.count, 0, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
-            else if (tr == TR_CULLED) launch_intersect<TR_CULLED, kBlk>(L.count, 0, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
-            else if (tr == TR_BVH) launch_intersect<TR_BVH, kBlk>(L.count, 0, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
-            else if (tr == TR_BVH2_LDS)
-                launch_intersect<TR_BVH2_LDS, kBlk>(L.count, kStackBytes + L.S.b2_lds_bytes, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
-            else if (tr == TR_BVH2_GLOBAL)
-                launch_intersect<TR_BVH2_GLOBAL, kBlk>(L.count, kStackBytes, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
-            else launch_intersect<TR_SBVH_GLOBAL, kBlk>(L.count, 0, st, L, G, B.q[cur][0], B.q[cur][1], cnt, B.hits);
-            const int nx = 1 - cur;
-            uint32_t* cnt_out = B.counts + (size_t)(bounce + 1) * nseg;
-            if (L.count)
-                hipLaunchKernelGGL(k_shade<true>, dim3(nseg), dim3(kBlk), 0, st, L.S, L.P, G, B.q[cur][0], B.q[cur][1],
-                                   B.q[cur][2], B.qr[cur], cnt, B.hits, B.q[nx][0], B.q[nx][1], B.q[nx][2], B.qr[nx], cnt_out,
-                                   B.res, B.res_id, L.counters);
-            else
-                hipLaunchKernelGGL(k_shade<false>, dim3(nseg), dim3(kBlk), 0, st, L.S, L.P, G, B.q[cur][0], B.q[cur][1],
-                                   B.q[cur][2], B.qr[cur], cnt, B.hits, B.q[nx][0], B.q[nx][1], B.q[nx][2], B.qr[nx], cnt_out,
-                                   B.res, B.res_id, L.counters);
-            cur = nx;
+        R.batch = b;
+        switch (tr) {
+            case TR_BRUTE: run_tr<TR_BRUTE>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
+            case TR_CULLED: run_tr<TR_CULLED>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
+            case TR_BVH: run_tr<TR_BVH>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
+            case TR_SBVH_GLOBAL: run_tr<TR_SBVH_GLOBAL>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
+            case TR_BVH2_LDS: run_tr<TR_BVH2_LDS>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
+            default: run_tr<TR_BVH2_GLOBAL>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
         }
         const uint32_t grid_a = (n_px + kBlk - 1) / kBlk;
         if (L.count)

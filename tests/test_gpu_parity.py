@@ -172,3 +172,21 @@ def test_pixel_list_shard_equals_full_frame(om, kernel):
     frame = shard.assemble(W, H, shards)
     nb, msg = compare_stats(frame, full.pixels, f"shards/{kernel}")
     assert nb == 0, msg
+
+
+@pytest.mark.parametrize("tail", [1, 2, 3, 7, 50])
+def test_tail_bounce_is_bit_identical(om, oracle, tail):
+    """Wavefront scheduling knob: any tail bounce (persistent whole-path launch) == oracle."""
+    from raytracingoneweekend_amd import _lib as L
+    W, H, SPP = 48, 30, 4
+    world = om.random_scene(0x5EED, with_torus=True)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam, kernel="auto", pipeline="wavefront")
+    L.check(L.lib.om_set_tail_bounce(fz.ctx, tail), fz.ctx)
+    pix = om.PixelsBox.new(W * H)
+    c = om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=9)
+    p = oracle.params(W, H, SPP, max_depth=50, seed=9)
+    exp, _ = oracle.render(oracle.random_scene(0x5EED, with_torus=True), oracle.default_camera(W / H), p)
+    nb, msg = compare_stats(pix.pixels, exp, f"tail{tail}")
+    assert nb == 0, msg
+    assert c["samples"] == W * H * SPP
