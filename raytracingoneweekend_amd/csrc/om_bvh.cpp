@@ -118,7 +118,9 @@ struct Builder {
             }
         }
         const double leaf_cost = bb.area() * count;
-        const double trav = 1.0 * bb.area();  // traversal cost relative to one primitive test
+        // traversal cost relative to one primitive test; leaves <= 8 (a sweep of cost 0.3-2
+        // and max leaf 2-8 moved C1 by < 1%: the tree is not what bounds the kernel)
+        const double trav = 1.0 * bb.area();
         if (best_axis < 0 || depth >= kSahDepth) {
             if (count <= 4 || (best_axis < 0 && count <= 8)) return make_leaf();
             // degenerate centroids: median split on the longest box axis
@@ -199,6 +201,21 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     for (size_t i = 0; i < w.parallelograms.size(); ++i) always.push_back(fw.offsets[K_PARA] + (uint32_t)i);
     std::sort(always.begin(), always.end());
     fw.always2 = always;
+    fw.always2_rec.clear();
+    for (uint32_t gi : always) {
+        OmAlwaysRec r;
+        r.gi = gi; r.pad = 0;
+        Box bx;
+        bool bounded = true;
+        if (gi >= fw.offsets[K_TRI] && gi < fw.offsets[K_TRI + 1]) bx = bary_box(w.triangles[gi - fw.offsets[K_TRI]], false);
+        else if (gi >= fw.offsets[K_PARA] && gi < fw.offsets[K_PARA + 1]) bx = bary_box(w.parallelograms[gi - fw.offsets[K_PARA]], true);
+        else bounded = false;   // planes; huge spheres/cubes (their inflation would cover the scene)
+        for (int i = 0; i < 3; ++i) {
+            r.lo[i] = bounded ? std::nextafter((float)bx.lo[i], -INFINITY) : -INFINITY;
+            r.hi[i] = bounded ? std::nextafter((float)bx.hi[i], INFINITY) : INFINITY;
+        }
+        fw.always2_rec.push_back(r);
+    }
     fw.snodes.clear();
     fw.srecs.clear();
     if (b.items.empty()) return;

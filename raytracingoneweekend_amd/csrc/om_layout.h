@@ -97,6 +97,15 @@ struct OM_ALIGN16 OmSkipNode {
     uint32_t leaf;
 };
 
+// Prim tested outside the BVH2 tree (always2), with a conservative box tested first:
+// inflated for triangles/parallelograms, infinite for planes and huge bounds.
+struct OM_ALIGN16 OmAlwaysRec {
+    float lo[3];
+    uint32_t gi;
+    float hi[3];
+    uint32_t pad;
+};
+
 // Compressed binary BVH node (64 B): both child boxes live in the parent, so one
 // node read yields both slab tests.  child = 16-bit code: node index, or
 // OM_LEAF | leaf index; b2leaves[leaf] = (first_record << 8) | count (records =
@@ -136,6 +145,7 @@ struct OmSceneDev {
     // compressed BVH2 over the same leaves/records as the stackless BVH
     const OmBvh2Node* b2nodes;
     const uint32_t* b2leaves;
+    const OmAlwaysRec* always2_rec;  // always2 with boxes (BVH2 traversal)
     uint32_t n_b2nodes, n_b2leaves;
     uint32_t b2_lds_bytes;        // node bytes when they fit the LDS budget, else 0 (global nodes)
 };

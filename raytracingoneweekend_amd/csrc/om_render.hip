@@ -483,7 +483,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     UP(tri, tri); UP(plane, plane); UP(para, para);
     UP(msph, msph); UP(mbox, mbox); UP(mtor, mtor);
     UP(mats, mats); UP(bloom, bloom); UP(bvh, bvh); UP(bvh_prims, bvh_prims); UP(always, always);
-    UP(snodes, snodes); UP(srecs, srecs); UP(always2, always2); UP(b2nodes, b2nodes); UP(b2leaves, b2leaves);
+    UP(snodes, snodes); UP(srecs, srecs); UP(always2, always2); UP(always2_rec, always2_rec); UP(b2nodes, b2nodes); UP(b2leaves, b2leaves);
 #undef UP
     S.n_sph = fw.counts[0]; S.n_cube = fw.counts[1]; S.n_tri = fw.counts[2]; S.n_plane = fw.counts[3]; S.n_para = fw.counts[4];
     S.n_msph = fw.counts[5]; S.n_mbox = fw.counts[6]; S.n_mtor = fw.counts[7];

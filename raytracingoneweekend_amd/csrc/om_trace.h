@@ -140,12 +140,22 @@ __device__ __forceinline__ int traced_sbvh(const OmSceneDev& S, const OmSkipNode
                                            F3 o, F3 d, float tmin, float& closest, Wk& w) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return traced_brute<false, Wk>(S, o, d, tmin, closest, w);
     int best = -1;
-    for (uint32_t k = 0; k < S.n_always2; ++k) offer(S, S.always2[k], o, d, tmin, closest, best, w);
     const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
     const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
     const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
+    for (uint32_t k = 0; k < S.n_always2; ++k) {      // box first, then the exact test
+        const OmAlwaysRec A = S.always2_rec[k];
+        w.add_pre();
+        const float t_hi = closest * 1.0001f + 1e-3f;
+        const float x0 = __builtin_fmaf(A.lo[0], ix, nox), x1 = __builtin_fmaf(A.hi[0], ix, nox);
+        const float y0 = __builtin_fmaf(A.lo[1], iy, noy), y1 = __builtin_fmaf(A.hi[1], iy, noy);
+        const float z0 = __builtin_fmaf(A.lo[2], iz, noz), z1 = __builtin_fmaf(A.hi[2], iz, noz);
+        const float n0 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+        const float f0 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        if (!(n0 > f0)) offer(S, A.gi, o, d, tmin, closest, best, w);
+    }
     const uint32_t n = S.n_snodes;
     uint32_t node = 0;
     while (node < n) {
@@ -314,12 +324,22 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
                                            F3 o, F3 d, float tmin, float& closest, Wk& w) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
-    for (uint32_t k = 0; k < S.n_always2; ++k) offer(S, S.always2[k], o, d, tmin, closest, best, w);
     const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
     const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
     const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
+    for (uint32_t k = 0; k < S.n_always2; ++k) {      // box first, then the exact test
+        const OmAlwaysRec A = S.always2_rec[k];
+        w.add_pre();
+        const float t_hi = closest * 1.0001f + 1e-3f;
+        const float x0 = __builtin_fmaf(A.lo[0], ix, nox), x1 = __builtin_fmaf(A.hi[0], ix, nox);
+        const float y0 = __builtin_fmaf(A.lo[1], iy, noy), y1 = __builtin_fmaf(A.hi[1], iy, noy);
+        const float z0 = __builtin_fmaf(A.lo[2], iz, noz), z1 = __builtin_fmaf(A.hi[2], iz, noz);
+        const float n0 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+        const float f0 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        if (!(n0 > f0)) offer(S, A.gi, o, d, tmin, closest, best, w);
+    }
     const OmAffineTest* recs = S.srecs;
     uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
     int sp = 0;
