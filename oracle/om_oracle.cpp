@@ -13,7 +13,7 @@
 //   * The reference ships no tests, golden vectors or fixtures.
 //   * Its RNG is rand 0.8 ThreadRng (ChaCha12, OS-seeded; utils.rs:25) and is not
 //     reproducible, so the build defines its own counter-based RNG contract
-//     (om-rng v1) at exactly the reference's draw sites.
+//     (om-rng v2) at exactly the reference's draw sites.
 //   This restatement is therefore anchored by analytic known-answer tests
 //   (tests/test_oracle_kat.py) and by committed fixtures it generates
 //   (tests/golden/, made by tests/golden/make_golden.py).
@@ -40,8 +40,14 @@ static const float INF_F = INFINITY;
 static const float PI_F = 3.1415926535897932385f;  // utils.rs:29
 
 // ----------------------------------------------------------------------------
-// om-rng v1 (replaces rand::thread_rng(); utils.rs:25).  SplitMix64 stream;
-// f32 = top 24 bits * 2^-24 (rand 0.8 `Standard` f32 mapping, 24-bit grid).
+// om-rng v2 (replaces rand::thread_rng(); utils.rs:25).  Every draw maps 24 random
+// bits to f32 * 2^-24 (rand 0.8's `Standard` f32 mapping, a 24-bit grid in [0,1)).
+//   Rng      SplitMix64 — host-side streams: the scene generator and the jitter table.
+//   PathRng  the per-path stream used inside ray_color: a 32-bit Weyl counter s and a
+//            32-bit key k, both from one mix64 of (pixel << 32 | sample) ^ skey; a draw
+//            is lowbias32((s += 0x9E3779B9) ^ k) >> 8.  Two 32-bit multiplies per draw
+//            instead of SplitMix64's two 64-bit ones (~10% of the GPU bounce kernel);
+//            the key keeps two paths whose counters overlap uncorrelated.
 // ----------------------------------------------------------------------------
 static inline uint64_t mix64(uint64_t z) {
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
@@ -56,10 +62,23 @@ struct Rng {
     // utils.rs:26  rand_range(min,max) = rand()*(max-min) + min
     inline float rand_range(float mn, float mx) { float r = rand(); return r * (mx - mn) + mn; }
 };
+struct PathRng {
+    uint32_t s, k;
+    static inline PathRng from_state(uint64_t st) { PathRng r; r.s = (uint32_t)st; r.k = (uint32_t)(st >> 32); return r; }
+    inline uint32_t next_u32() {
+        s += 0x9E3779B9u;
+        uint32_t x = s ^ k;
+        x ^= x >> 16; x *= 0x21F0AAADu;
+        x ^= x >> 15; x *= 0x735A2D97u;
+        return x ^ (x >> 15);
+    }
+    inline float rand() { return (float)(next_u32() >> 8) * 5.9604644775390625e-8f; }            // utils.rs:25
+    inline float rand_range(float mn, float mx) { float r = rand(); return r * (mx - mn) + mn; }  // utils.rs:26
+};
 // Per-path stream: key = (pixel << 32) | sample, seed folded once.
 static inline uint64_t seed_key(uint64_t seed) { return mix64(seed + 0x632BE59BD9B4E019ULL); }
-static inline Rng path_rng(uint64_t skey, uint32_t pixel, uint32_t sample) {
-    Rng r; r.s = mix64((((uint64_t)pixel << 32) | (uint64_t)sample) ^ skey); return r;
+static inline PathRng path_rng(uint64_t skey, uint32_t pixel, uint32_t sample) {
+    return PathRng::from_state(mix64((((uint64_t)pixel << 32) | (uint64_t)sample) ^ skey));
 }
 
 // ----------------------------------------------------------------------------
@@ -100,16 +119,21 @@ static inline uint8_t f32_as_u8(float f) {
 static inline void to_u8x3(V3 c, uint8_t out[3]) {
     out[0] = f32_as_u8(c.x * 256.0f); out[1] = f32_as_u8(c.y * 256.0f); out[2] = f32_as_u8(c.z * 256.0f);
 }
-static inline V3 rand_v3_range(Rng& g, float mn, float mx) {                                 // vec3.rs:82-88
+template <class G>
+static inline V3 rand_v3_range(G& g, float mn, float mx) {                                 // vec3.rs:82-88
     float x = g.rand_range(mn, mx); float y = g.rand_range(mn, mx); float z = g.rand_range(mn, mx);
     return v3(x, y, z);
 }
-static inline V3 rand_v3(Rng& g) { float x = g.rand(); float y = g.rand(); float z = g.rand(); return v3(x, y, z); }  // vec3.rs:81
-static inline V3 rand_in_unit_sphere(Rng& g) {                                               // vec3.rs:92-97
+template <class G>
+static inline V3 rand_v3(G& g) { float x = g.rand(); float y = g.rand(); float z = g.rand(); return v3(x, y, z); }  // vec3.rs:81
+template <class G>
+static inline V3 rand_in_unit_sphere(G& g) {                                               // vec3.rs:92-97
     for (;;) { V3 p = rand_v3_range(g, -1.0f, 1.0f); if (length_squared(p) < 1.0f) return p; }
 }
-static inline V3 rand_unit_vector(Rng& g) { return unit(rand_in_unit_sphere(g)); }          // vec3.rs:98-100
-static inline V3 rand_in_unit_disc(Rng& g) {                                                 // vec3.rs:108-113
+template <class G>
+static inline V3 rand_unit_vector(G& g) { return unit(rand_in_unit_sphere(g)); }          // vec3.rs:98-100
+template <class G>
+static inline V3 rand_in_unit_disc(G& g) {                                                 // vec3.rs:108-113
     for (;;) {
         float x = g.rand_range(-1.0f, 1.0f); float y = g.rand_range(-1.0f, 1.0f);
         V3 p = v3(x, y, 0.0f);
@@ -527,7 +551,7 @@ static inline float reflectance(float cosv, float ref_idx) {                    
     float cos_5 = (1.0f - cosv) * (1.0f - cosv) * (1.0f - cosv) * (1.0f - cosv) * (1.0f - cosv);
     return r0_2 + (1.0f - r0_2) * cos_5;
 }
-static void scatter(const Ray& r_in, const HitRecord& hr, Rng& g, V3& atten, Ray& out) {   // materials.rs:39-51
+static void scatter(const Ray& r_in, const HitRecord& hr, PathRng& g, V3& atten, Ray& out) {   // materials.rs:39-51
     const Material& m = hr.material;
     if (m.type == MAT_LAMBERTIAN) {                                                          // :52-61
         V3 nd = hr.normal + rand_unit_vector(g);
@@ -568,7 +592,7 @@ static Camera camera_new(V3 lookfrom, V3 lookat, V3 vup, float vfov_deg, float a
     c.u = u; c.v = v; c.w = w; c.lens_radius = aperture / 2.0f; c.aspect = aspect; c.focus = focus; c.vw = vw; c.vh = vh;
     return c;
 }
-static Ray camera_get_ray(const Camera& c, float s, float t, Rng& g) {                      // camera.rs:60-65
+static Ray camera_get_ray(const Camera& c, float s, float t, PathRng& g) {                      // camera.rs:60-65
     V3 rl = c.lens_radius * rand_in_unit_disc(g);
     V3 offset = c.u * rl.x + c.v * rl.y;
     // uv_to_dir camera.rs:67-74 = cols (H, V, 0, llc-origin); dot with (u, v, 0, 1)
@@ -635,7 +659,7 @@ static bool stats_add(PixelStats& st, V3 x, float depth, uint64_t obj_id) {
 
 // handle_hit render_thread.rs:105-126 ; ray_color :128-143
 struct SampleResult { V3 color; float depth; uint64_t id; uint32_t segments; };
-static inline bool handle_hit(const World& w, Ray& r, V3& cur, float tmin, float tmax, Rng& g, float& depth, uint64_t& id) {
+static inline bool handle_hit(const World& w, Ray& r, V3& cur, float tmin, float tmax, PathRng& g, float& depth, uint64_t& id) {
     HitRecord hr;
     if (world_hit(w, r, tmin, tmax, hr)) {
         V3 att; Ray nr; scatter(r, hr, g, att, nr);
@@ -647,7 +671,7 @@ static inline bool handle_hit(const World& w, Ray& r, V3& cur, float tmin, float
     }
     return true;
 }
-static SampleResult ray_color(const World& w, Ray r, uint32_t depth, float tmin, float tmax, Rng& g) {
+static SampleResult ray_color(const World& w, Ray r, uint32_t depth, float tmin, float tmax, PathRng& g) {
     SampleResult out; V3 cur = v3(1.0f, 1.0f, 1.0f); out.segments = 1;
     float depthf; uint64_t obj_id;
     handle_hit(w, r, cur, tmin, tmax, g, depthf, obj_id);                                    // :132 (first_hit == hit, F5)
@@ -691,7 +715,7 @@ static void render_pixel(const World& w, const Camera& cam, const RenderParams& 
         if (p.adaptive && (st.flags & 1)) break;                                             // ThreadPixels::add_run :97-101
         uint32_t s = st.n;
         if (s >= p.spp_total) break;
-        Rng g = path_rng(skey, pxl, s);
+        PathRng g = path_rng(skey, pxl, s);
         float i_rand = (g.rand() + jt[2 * s]) / 2.0f;                                        // :188
         float j_rand = (g.rand() + jt[2 * s + 1]) / 2.0f;                                    // :189
         float u = (i_f + i_rand) / (wf - 1.0f);                                              // :190
@@ -795,7 +819,7 @@ void oro_world_torus(void* wp, uint32_t i, float* out) {
     st3(t.sizes, out + 40);
 }
 
-// --- front-end scene builders (main.rs:37-110), with om-rng v1 replacing thread_rng ---
+// --- front-end scene builders (main.rs:37-110), with SplitMix64 (om-rng Rng) replacing thread_rng ---
 // flags bit0: include the torus block main.rs:73-81 (S-full); S-traced omits it.
 // grid_half: 11 for random_scene (a,b in -11..11); 50 gives the S-10k variant (a,b in -50..50).
 // flags bit1: omit the parallelogram/triangle/cube blocks (S-10k: spheres + ground only).
@@ -883,7 +907,7 @@ static Camera cam_from(const OroCamera* c) {
 // --- RNG KAT surface ---
 void oro_rng_draws(uint64_t state, uint32_t n, float* out) { Rng g; g.s = state; for (uint32_t i = 0; i < n; ++i) out[i] = g.rand(); }
 void oro_rng_path_draws(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t n, float* out) {
-    Rng g = path_rng(seed_key(seed), pixel, sample); for (uint32_t i = 0; i < n; ++i) out[i] = g.rand();
+    PathRng g = path_rng(seed_key(seed), pixel, sample); for (uint32_t i = 0; i < n; ++i) out[i] = g.rand();
 }
 void oro_jitter_table(uint64_t seed, uint32_t spp, float* out) { auto jt = jitter_table(seed, spp); std::memcpy(out, jt.data(), jt.size() * 4); }
 uint64_t oro_bloom_hash(uint64_t id) { return bloom_hash(id); }
@@ -902,11 +926,11 @@ int oro_hit_world(void* wp, const float* ray6, float tmin, float tmax, float* ou
 void oro_scatter(const float* ray6, const float* hit7 /*t,p3,n3*/, const OroMaterial* m, uint64_t state, float* out, uint64_t* state_out) {
     Ray r; r.orig = ld3(ray6); r.dir = ld3(ray6 + 3);
     HitRecord h; h.t = hit7[0]; h.point = ld3(hit7 + 1); h.normal = ld3(hit7 + 4); h.material = to_mat(m); h.obj_id = 0;
-    Rng g; g.s = state; V3 att; Ray o; scatter(r, h, g, att, o);
+    PathRng g = PathRng::from_state(state); V3 att; Ray o; scatter(r, h, g, att, o);
     st3(att, out); st3(o.orig, out + 3); st3(o.dir, out + 6); *state_out = g.s;
 }
 void oro_get_ray(const OroCamera* c, float u, float v, uint64_t state, float* out6) {
-    Camera cam = cam_from(c); Rng g; g.s = state; Ray r = camera_get_ray(cam, u, v, g);
+    Camera cam = cam_from(c); PathRng g = PathRng::from_state(state); Ray r = camera_get_ray(cam, u, v, g);
     st3(r.orig, out6); st3(r.dir, out6 + 3);
 }
 void oro_stats_add(void* st, const float* color, float depth, uint64_t id) { stats_add(*(PixelStats*)st, ld3(color), depth, id); }

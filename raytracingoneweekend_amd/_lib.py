@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libottomarcher.so")
+# OM_LIB: load another build of the same library (A/B timing of build variants, tools/ablate.sh)
+LIB_PATH = os.environ.get("OM_LIB") or os.path.join(_HERE, "libottomarcher.so")
 
 OM_OK = 0
 OM_ERR_INVALID, OM_ERR_DEVICE, OM_ERR_STATE, OM_ERR_UNSUPPORTED, OM_ERR_NOMEM = -1, -2, -3, -4, -5

@@ -40,17 +40,20 @@ __device__ __forceinline__ F3 xform_v(const float* m, const float* z, F3 p) {
               m[8] * p.x + m[9] * p.y + m[10] * p.z + z[2]);
 }
 
-// ---------------------------------------------------------------- om-rng v1
-// SplitMix64; f32 = (z >> 40) * 2^-24.  Replaces rand::thread_rng() (utils.rs:25).
+// ---------------------------------------------------------------- om-rng v2
+// Per-path stream (replaces rand::thread_rng(), utils.rs:25): 32-bit Weyl counter s and
+// 32-bit key k from one mix64 of (pixel << 32 | sample) ^ skey; a draw is
+// lowbias32((s += 0x9E3779B9) ^ k) >> 8, times 2^-24 (rand 0.8's 24-bit f32 grid).
+// Same as PathRng in oracle/om_oracle.cpp.
 struct Rng {
-    uint64_t s;
+    uint32_t s, k;
     __device__ __forceinline__ float next() {
-        s += 0x9E3779B97F4A7C15ULL;
-        uint64_t z = s;
-        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
-        z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
-        z ^= z >> 31;
-        return (float)(uint32_t)(z >> 40) * 5.9604644775390625e-8f;
+        s += 0x9E3779B9u;
+        uint32_t x = s ^ k;
+        x ^= x >> 16; x *= 0x21F0AAADu;
+        x ^= x >> 15; x *= 0x735A2D97u;
+        x ^= x >> 15;
+        return (float)(x >> 8) * 5.9604644775390625e-8f;
     }
     __device__ __forceinline__ float range(float lo, float hi) { const float r = next(); return r * (hi - lo) + lo; }  // utils.rs:26
 };
@@ -60,7 +63,8 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
     return z ^ (z >> 31);
 }
 __device__ __forceinline__ Rng path_rng(uint64_t skey, uint32_t pixel, uint32_t sample) {
-    Rng r; r.s = mix64((((uint64_t)pixel << 32) | (uint64_t)sample) ^ skey); return r;
+    const uint64_t z = mix64((((uint64_t)pixel << 32) | (uint64_t)sample) ^ skey);
+    Rng r; r.s = (uint32_t)z; r.k = (uint32_t)(z >> 32); return r;
 }
 __device__ __forceinline__ F3 rand_in_unit_sphere(Rng& g) {                                      // vec3.rs:92-97
     for (;;) {

@@ -159,7 +159,7 @@ struct OmCamDev {
 struct OmParamsDev {
     uint32_t width, height, spp_total, sample_count, max_depth, march_steps, adaptive;
     float tmin, tmax, wf_m1, hf_m1;   // (W-1), (H-1) as f32
-    uint64_t skey;                     // mix64(seed + K) (om-rng v1)
+    uint64_t skey;                     // mix64(seed + K) (om-rng v2 path key)
     uint32_t n_pixels;                 // pixels this launch covers
     uint32_t tiles_x;                  // 8x8 tiles per row (full-frame mapping)
 };

@@ -105,7 +105,7 @@ __global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(O
     uint32_t todo = valid ? P.sample_count : 0u;
     bool live = false;
     F3 o = f3(0, 0, 0), d = f3(0, 0, 0), cur = f3(1, 1, 1);
-    Rng g; g.s = 0;
+    Rng g; g.s = 0; g.k = 0;
     uint32_t seg = 0, first_id = 0;
     float depthf = 0.0f;
     WorkT<COUNT> w;
@@ -289,7 +289,7 @@ om_status ensure(om_ctx* c, DevBuf& b, size_t n) {
     return OM_OK;
 }
 
-// jitter table render_thread.rs:164-174: ((s/2)&1, s&1) shuffled once (om-rng v1 Fisher-Yates)
+// jitter table render_thread.rs:164-174: ((s/2)&1, s&1) shuffled once (om-rng SplitMix64 Fisher-Yates)
 om_status prepare_jitter(om_ctx* c, uint64_t seed, uint32_t spp) {
     if (c->jitter.p && c->jitter_seed == seed && c->jitter_spp == spp) return OM_OK;
     std::vector<float> jt(2 * (size_t)spp);

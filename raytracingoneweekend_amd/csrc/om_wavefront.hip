@@ -91,7 +91,7 @@ struct Seg {
     uint32_t segcap;  // paths per segment
 };
 
-// One SoA path queue: o|depthf, d|first_id, throughput|segment, rng lo|rng hi|slot|-.
+// One SoA path queue: o|depthf, d|first_id, throughput|segment, rng s|rng k|slot|-.
 struct Queue {
     float4* q0; float4* q1; float4* q2; uint4* qr;
 };
@@ -122,13 +122,13 @@ __device__ __forceinline__ void load_rest(const Queue& Q, uint64_t i, Path& p) {
     const float4 c = Q.q2[i];
     const uint4 r = Q.qr[i];
     p.cur = f3(c.x, c.y, c.z); p.seg = __float_as_uint(c.w);
-    p.g.s = ((uint64_t)r.y << 32) | r.x; p.slot = r.z;
+    p.g.s = r.x; p.g.k = r.y; p.slot = r.z;
 }
 __device__ __forceinline__ void store_path(const Queue& Q, uint64_t i, const Path& p) {
     Q.q0[i] = make_float4(p.o.x, p.o.y, p.o.z, p.depthf);
     Q.q1[i] = make_float4(p.d.x, p.d.y, p.d.z, __uint_as_float(p.first_id));
     Q.q2[i] = make_float4(p.cur.x, p.cur.y, p.cur.z, __uint_as_float(p.seg));
-    Q.qr[i] = make_uint4((uint32_t)p.g.s, (uint32_t)(p.g.s >> 32), p.slot, 0u);
+    Q.qr[i] = make_uint4(p.g.s, p.g.k, p.slot, 0u);
 }
 
 // Scene data a workgroup traces against: BVH2 nodes + leaf table staged in LDS behind

@@ -22,7 +22,7 @@ om_status fail(om_status code, const char* msg) {
     return code;
 }
 
-// ---- om-rng v1 (host side).  Replaces rand::thread_rng() (utils.rs:25).
+// ---- om-rng SplitMix64 (host side: scene + jitter).  Replaces rand::thread_rng() (utils.rs:25).
 struct SplitMix {
     uint64_t s;
     static uint64_t mix(uint64_t z) {
@@ -411,7 +411,7 @@ om_status om_world_export(const om_world* w, int32_t kind, uint32_t i, float* ou
     return fail(OM_ERR_INVALID, "om_world_export: unsupported kind");
 }
 
-// main.rs:37-100 with om-rng v1 in place of thread_rng.
+// main.rs:37-100 with om-rng SplitMix64 in place of thread_rng.
 om_status om_world_random_scene(om_world* w, uint64_t seed, uint32_t flags, int32_t grid_half) {
     if (!w || grid_half < 0 || grid_half > 4096) return fail(OM_ERR_INVALID, "om_world_random_scene: bad arguments");
     SplitMix g{seed};

@@ -5,7 +5,7 @@
   * random_scene_api(seed) -> the same scene composed through the Python mirror of the
                               reference API (Material / m4x4 / Sphere.new / `world +=`),
                               exactly as main.rs writes it; tests assert both agree bit for bit.
-Both draw from om-rng v1 (SplitMix64) in the reference's draw order.
+Both draw from om-rng's SplitMix64 host stream in the reference's draw order.
 """
 import numpy as np
 
@@ -22,7 +22,7 @@ S_FULL = 1            # random_scene exactly as main.rs:37-100 (torus included)
 
 
 class SplitMix64:
-    """om-rng v1 stream (replaces rand::thread_rng, utils.rs:25)."""
+    """om-rng host stream (SplitMix64) (replaces rand::thread_rng, utils.rs:25)."""
 
     M = (1 << 64) - 1
 

@@ -1,4 +1,4 @@
-"""Generates tests/golden/golden_v1.npz with the CPU oracle (oracle/om_oracle.cpp).
+"""Generates tests/golden/golden_v2.npz with the CPU oracle (oracle/om_oracle.cpp).
 
 The reference ships no golden vectors and cannot be built here (no Rust toolchain), so
 these fixtures pin the oracle against drift and give the GPU tests a stored answer.
@@ -51,6 +51,6 @@ def build(O):
 if __name__ == "__main__":
     from oracle import oracle as O
     g = build(O)
-    out = os.path.join(HERE, "golden_v1.npz")
+    out = os.path.join(HERE, "golden_v2.npz")
     np.savez_compressed(out, **g)
     print("wrote", out, os.path.getsize(out), "bytes")

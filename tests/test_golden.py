@@ -1,4 +1,4 @@
-"""Committed fixtures (tests/golden/golden_v1.npz, made by tests/golden/make_golden.py):
+"""Committed fixtures (tests/golden/golden_v2.npz, made by tests/golden/make_golden.py):
 the oracle must keep reproducing them (CPU), and the HIP path must produce the stored
 images bit for bit (GPU) — no oracle needed at GPU run time."""
 import os
@@ -8,7 +8,7 @@ import pytest
 
 from scenes_common import kitchen_sink
 
-G = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_v1.npz"))
+G = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_v2.npz"))
 
 
 def test_oracle_reproduces_rng_and_tables(oracle):

@@ -22,6 +22,47 @@ def test_rng_matches_product_python_stream(oracle):
     assert np.array_equal(oracle.rng_draws(0x5EED, 50), np.array([g.rand() for _ in range(50)], dtype=F))
 
 
+def _path_draws_py(seed, pixel, sample, n):
+    """om-rng v2 path stream restated in Python."""
+    M = (1 << 64) - 1
+
+    def mix64(z):
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return z ^ (z >> 31)
+
+    skey = mix64((seed + 0x632BE59BD9B4E019) & M)
+    return _path_state_draws_py(mix64(((pixel << 32) | sample) ^ skey), n)
+
+
+def _path_state_draws_py(state, n):
+    s, k = state & 0xFFFFFFFF, state >> 32
+    out = []
+    for _ in range(n):
+        s = (s + 0x9E3779B9) & 0xFFFFFFFF
+        x = s ^ k
+        x ^= x >> 16
+        x = (x * 0x21F0AAAD) & 0xFFFFFFFF
+        x ^= x >> 15
+        x = (x * 0x735A2D97) & 0xFFFFFFFF
+        x ^= x >> 15
+        out.append((x >> 8) / 2 ** 24)
+    return np.array(out, dtype=F)
+
+
+@pytest.mark.parametrize("seed,pixel,sample", [(1, 0, 0), (1, 12345, 7), (0x5EED, 2073599, 511), (2 ** 63, 7, 2 ** 31)])
+def test_path_stream_matches_python_restatement(oracle, seed, pixel, sample):
+    assert np.array_equal(oracle.path_draws(seed, pixel, sample, 64), _path_draws_py(seed, pixel, sample, 64))
+
+
+def test_path_stream_uniformity(oracle):
+    d = np.concatenate([oracle.path_draws(1, p, s, 16) for p in range(64) for s in range(16)]).astype(np.float64)
+    assert np.all(d * 2 ** 24 == np.floor(d * 2 ** 24)) and (d >= 0).all() and (d < 1).all()
+    assert abs(d.mean() - 0.5) < 0.01
+    hist, _ = np.histogram(d, bins=16, range=(0, 1))
+    assert hist.min() > 0.85 * d.size / 16
+
+
 def test_draws_on_24bit_grid(oracle):
     d = oracle.rng_draws(12345, 4096).astype(np.float64)
     assert (d >= 0).all() and (d < 1).all()
@@ -137,7 +178,7 @@ def test_dielectric_schlick_normal_incidence(oracle):
     mat = oracle.material("dielectric", ior=1.5)
     lo = hi = None
     for s in range(2000):
-        u = oracle.rng_draws(s, 1)[0]
+        u = _path_state_draws_py(s, 1)[0]     # oro_scatter draws from om-rng's path stream
         if u < 0.04 and lo is None:
             lo = s
         if u > 0.5 and hi is None:
