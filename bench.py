@@ -38,14 +38,19 @@ PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md; FMA = 2 fl
 PEAK_HBM_GBS = 8000.0
 
 # Algorithmic FP32 work per counted unit, counted from om_device.h /
-# om_render.hip in the reference's op order (no FMA: every add/mul/div/sqrt/min/max/cmp = 1).
+# om_trace.h in the reference's op order (no FMA: every add/mul/div/sqrt/min/max/cmp = 1).
 FLOP_EXACT_TEST = 56      # Sphere::hit miss path: 2 affine xforms (36) + a, half_b, c, disc, cmp (20)
 FLOP_BOX_TEST = 25        # slab test of one BVH child box
 FLOP_SEGMENT = 110        # finalize (point + normal) + scatter + throughput + loop bookkeeping
-FLOP_SAMPLE = 95          # jitter/uv + lens disc + get_ray + Stats::add
+FLOP_CAMERA_RAY = 50      # jitter/uv + lens disc + get_ray (bounce 0, once per sample)
 FLOP_MARCH_STEP = 60      # one sphere-tracing iteration over the marched objects (S-traced: none)
-# HBM bytes per unit: Stats read + write once per pixel per launch (40 B each way)
-BYTES_PER_PIXEL_LAUNCH = 80
+# Algorithmic HBM bytes of the bounce kernels (SoA path queue): a segment
+# after the first reads its 64-B path and writes the 64-B survivor; a sample reads its
+# pixel id + Stats.n/flags (12 B) and writes its result (20 B).
+BYTES_PER_LATER_SEGMENT = 128
+BYTES_PER_SAMPLE = 32
+BOUNCE_FAMILY = ("bounce0", "bounce", "tail")            # one fused trace+shade kernel body
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
 def cpu_baseline(budget_s=12.0):
@@ -78,6 +83,7 @@ def main():
     ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
     ap.add_argument("--pipeline", default="wavefront", choices=list(L.PIPELINES))
     ap.add_argument("--tail", type=int, default=0, help="first bounce of the persistent tail launch (0 = library default)")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -123,7 +129,6 @@ def main():
         step(p)
     torch.cuda.synchronize()
     stats.zero_()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     gathered, send = None, None
     if world_size > 1:                                       # gather buffers (equal-size shards), allocated untimed
         n_max = shard.shard_capacity(W, H, world_size) * 40
@@ -131,15 +136,17 @@ def main():
         gathered = [torch.empty_like(send) for _ in range(world_size)] if rank == 0 else None
     torch.cuda.synchronize()
 
+    kt = L.om_kernel_times()
+    timing = not args.no_kernel_timing
+    L.check(L.lib.om_set_timing(ctx, int(timing)), ctx)      # HIP events around every launch, on `stream`
+
     # ---- timed region
     if world_size > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        ev[k][0].record(stream)
         step(p)
-        ev[k][1].record(stream)
     if world_size > 1:                                       # RCCL gather of the f32 framebuffer to rank 0
         send[: stats.numel()] = stats
         dist.gather(send, gathered, dst=0)
@@ -153,7 +160,8 @@ def main():
     if world_size > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    launch_ms = [a.elapsed_time(b) for a, b in ev]
+    L.check(L.lib.om_get_kernel_times(ctx, C.byref(kt)), ctx)
+    L.check(L.lib.om_set_timing(ctx, 0), ctx)
     host = stats.cpu().numpy().view(L.PIXEL_STATS_DTYPE).copy()
     assert int(host["n"].min()) == spp_total and int(host["n"].max()) == spp_total, "every pixel must take every sample"
 
@@ -172,12 +180,34 @@ def main():
     total_samples = W * H * spp_total                          # all ranks together
     value = total_samples / elapsed / 1e6
 
-    # roofline of the dominant kernel (render_kernel), per launch, from the live counters
-    avg_launch_s = float(np.mean(launch_ms)) / 1e3
-    flops = (FLOP_EXACT_TEST * ctr.prim_tests + FLOP_BOX_TEST * ctr.pre_tests + FLOP_SEGMENT * ctr.segments
-             + FLOP_SAMPLE * ctr.samples + FLOP_MARCH_STEP * ctr.march_steps) / args.steps
-    achieved_tflops = flops / avg_launch_s / 1e12
-    hbm_gbs = BYTES_PER_PIXEL_LAUNCH * n_px / avg_launch_s / 1e9
+    # roofline of the dominant kernel: the fused trace+shade bounce kernel (all its launches:
+    # bounce 0, bounces 1.., tail), algorithmic flops from the live counters / its event time
+    fam = [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
+    if args.pipeline == "megakernel":
+        fam = [L.KT_CLASSES.index("megakernel")]
+    launches = sum(kt.launches[i] for i in fam)
+    kern_s = sum(kt.ms[i] for i in fam) / 1e3
+    roof = None
+    if timing and launches:
+        flops = (FLOP_EXACT_TEST * ctr.prim_tests + FLOP_BOX_TEST * ctr.pre_tests + FLOP_SEGMENT * ctr.segments
+                 + FLOP_CAMERA_RAY * ctr.samples + FLOP_MARCH_STEP * ctr.march_steps)
+        nbytes = BYTES_PER_LATER_SEGMENT * (ctr.segments - ctr.samples) + BYTES_PER_SAMPLE * ctr.samples
+        avg_launch_s = kern_s / launches
+        achieved_tflops = flops / kern_s / 1e12
+        traffic, traffic_src = None, None
+        if os.path.exists(PMC_TRAFFIC) and args.pipeline == "wavefront" and args.kernel == "auto":
+            pm = json.load(open(PMC_TRAFFIC))
+            traffic, traffic_src = pm["hbm_bytes_per_launch"], pm["source"]
+        roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": traffic,
+                "kernel": "k_bounce0+k_bounce+k_tail (fused trace+shade)" if args.pipeline == "wavefront" else "render_kernel",
+                "launches_per_step": round(launches / args.steps, 2), "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                "flop_per_launch": round(flops / launches), "algorithmic_bytes_per_launch": round(nbytes / launches),
+                "hbm_achieved_gbs": round(nbytes / kern_s / 1e9, 2), "traffic_source": traffic_src,
+                "kernel_share_of_step": round(kern_s / elapsed, 4),
+                "all_kernels_ms_per_step": {k: round(kt.ms[i] / args.steps, 4) for i, k in enumerate(L.KT_CLASSES)
+                                            if kt.launches[i]}}
+    hbm_gbs = roof["hbm_achieved_gbs"] if roof else None
 
     if rank == 0:
         if gathered is not None:                             # assemble + verify the gathered frame (untimed)
@@ -203,11 +233,8 @@ def main():
                        "width": W, "height": H, "spp_per_step": spp_step, "max_depth": MAX_DEPTH,
                        "parallelism": f"tile{world_size}", "kernel": args.kernel, "pipeline": args.pipeline,
                        "tail_bounce": args.tail or "default"},
-            "hbm_gbs": round(hbm_gbs, 2),
-            "roofline": {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS,
-                         "unit": "TFLOP/s", "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": None,
-                         "kernel": "render_kernel", "avg_launch_ms": round(avg_launch_s * 1e3, 4),
-                         "flop_per_launch": flops},
+            "hbm_gbs": hbm_gbs,
+            "roofline": roof,
             "work": {"segments_per_sample": round(ctr.segments / max(1, ctr.samples), 4),
                      "prim_tests_per_segment": round(ctr.prim_tests / max(1, ctr.segments), 3),
                      "box_tests_per_segment": round(ctr.pre_tests / max(1, ctr.segments), 3),

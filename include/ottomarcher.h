@@ -211,6 +211,25 @@ om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
  * scheduling knob: results are bit-identical for every value. */
 om_status om_set_tail_bounce(om_ctx* ctx, uint32_t bounce);
 
+/* Per-kernel-class device time: while enabled, every launch is bracketed by a HIP event
+ * pair on its stream (bench.py's roofline uses it).  om_get_kernel_times synchronises
+ * the last recorded event, returns the totals since the previous read (or since
+ * om_set_timing) and clears them.  Classes: */
+enum {
+    OM_KT_BOUNCE0 = 0,     /* wavefront bounce 0: camera rays + trace + shade + compact   */
+    OM_KT_BOUNCE = 1,      /* wavefront bounce b >= 1: trace + shade + compact              */
+    OM_KT_TAIL = 2,        /* wavefront persistent tail (bounces >= om_set_tail_bounce)   */
+    OM_KT_ACCUMULATE = 3,  /* wavefront Stats::add in sample order                          */
+    OM_KT_MEGAKERNEL = 4,  /* megakernel pipeline: one launch per render call              */
+    OM_KT_N = 5
+};
+typedef struct om_kernel_times {
+    uint64_t launches[OM_KT_N];
+    double ms[OM_KT_N];
+} om_kernel_times;
+om_status om_set_timing(om_ctx* ctx, int32_t enable);
+om_status om_get_kernel_times(om_ctx* ctx, om_kernel_times* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,6 +45,13 @@ class om_counters(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("samples", "segments", "prim_tests", "pre_tests", "march_steps", "credited")]
 
 
+KT_CLASSES = ("bounce0", "bounce", "tail", "accumulate", "megakernel")   # OM_KT_* order
+
+
+class om_kernel_times(C.Structure):
+    _fields_ = [("launches", C.c_uint64 * 5), ("ms", C.c_double * 5)]
+
+
 # numpy view of om_pixel_stats (40 B) — render_thread.rs:9-17
 PIXEL_STATS_DTYPE = np.dtype([("bloom", "<u8"), ("sum", "<f4", (3,)), ("n", "<u4"), ("avg_depth", "<f4"),
                               ("bad_avgs", "<u4"), ("color", "u1", (3,)), ("flags", "u1"), ("reserved", "<u4")])
@@ -62,7 +69,7 @@ EXPORTS = [
     "om_world_random_scene", "om_world_basic_scene", "om_world_marched_scene", "om_create", "om_destroy",
     "om_last_error", "om_upload_world", "om_set_kernel", "om_render", "om_render_device",
     "om_render_device_pixels", "om_get_counters", "om_reset_counters", "om_set_counting", "om_set_pipeline",
-    "om_set_tail_bounce",
+    "om_set_tail_bounce", "om_set_timing", "om_get_kernel_times",
 ]
 
 
@@ -138,6 +145,8 @@ def _load():
         "om_set_counting": (st, [vp, C.c_int32]),
         "om_set_pipeline": (st, [vp, C.c_int32]),
         "om_set_tail_bounce": (st, [vp, C.c_uint32]),
+        "om_set_timing": (st, [vp, C.c_int32]),
+        "om_get_kernel_times": (st, [vp, C.POINTER(om_kernel_times)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

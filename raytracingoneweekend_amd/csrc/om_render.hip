@@ -244,6 +244,7 @@ struct om_ctx {
     bool count_work = true;
     int pipeline = OM_PIPELINE_WAVEFRONT;
     uint32_t tail_bounce = 0;
+    omw::Timer timer;
     omw::Buffers wf;
     DevBuf frame_list;                  // tile-ordered pixel list of the full frame (wavefront path)
     uint32_t frame_w = 0, frame_h = 0;
@@ -251,6 +252,7 @@ struct om_ctx {
         for (auto& b : scene_bufs) b.release();
         counters.release(); jitter.release(); stats.release(); pixels.release(); frame_list.release();
         wf.release();
+        timer.release();
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -382,6 +384,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         L.counters = (unsigned long long*)c->counters.p;
         L.count = c->count_work;
         L.tail_bounce = c->tail_bounce;
+        L.timer = &c->timer;
         L.trace_mode = mode == OM_KERNEL_BRUTE ? MODE_BRUTE : mode == OM_KERNEL_CULLED ? MODE_CULLED
                      : mode == OM_KERNEL_BVH ? MODE_BVH : mode == OM_KERNEL_BVH2 ? 6 : MODE_SBVH_LDS;
         if (dev_pixels) {
@@ -412,6 +415,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     const float2* jt = (const float2*)c->jitter.p;
     unsigned long long* ctr = (unsigned long long*)c->counters.p;
     const bool count = c->count_work;
+    c->timer.begin(stream);
     if (mode == OM_KERNEL_SBVH) {
         if (c->scene.lds_bytes)
             go<MODE_SBVH_LDS, kBlockLds>(count, threads, c->scene.lds_bytes, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
@@ -424,6 +428,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     } else {
         go<MODE_BVH, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
     }
+    c->timer.end(OM_KT_MEGAKERNEL, stream);
     OM_HIP(c, hipGetLastError());
     return OM_OK;
 }
@@ -576,6 +581,33 @@ om_status om_set_pipeline(om_ctx* c, int32_t pipeline) {
 om_status om_set_tail_bounce(om_ctx* c, uint32_t bounce) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
     c->tail_bounce = bounce;
+    return OM_OK;
+}
+
+om_status om_set_timing(om_ctx* c, int32_t enable) {
+    if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
+    OM_HIP(c, hipSetDevice(c->device));
+    if (!enable && c->timer.on && !c->timer.cls.empty()) {
+        OM_HIP(c, hipEventSynchronize(c->timer.ev[2 * c->timer.cls.size() - 1]));
+    }
+    c->timer.on = enable != 0;
+    c->timer.cls.clear();
+    return OM_OK;
+}
+
+om_status om_get_kernel_times(om_ctx* c, om_kernel_times* out) {
+    if (!c || !out) return set_err(c, OM_ERR_INVALID, "om_get_kernel_times: null argument");
+    OM_HIP(c, hipSetDevice(c->device));
+    *out = om_kernel_times{};
+    omw::Timer& t = c->timer;
+    if (!t.cls.empty()) OM_HIP(c, hipEventSynchronize(t.ev[2 * t.cls.size() - 1]));
+    for (size_t i = 0; i < t.cls.size(); ++i) {
+        float ms = 0.0f;
+        OM_HIP(c, hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
+        out->launches[t.cls[i]] += 1u;
+        out->ms[t.cls[i]] += (double)ms;
+    }
+    t.cls.clear();
     return OM_OK;
 }
 

@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <string>
+#include <vector>
 
 #include "../../include/ottomarcher.h"
 #include "om_layout.h"
@@ -22,6 +23,30 @@ struct Buffers {
     void release();
 };
 
+// Optional per-launch device timing (om_set_timing): a begin/end HIP event pair recorded
+// on the launch stream around every kernel, tagged with its OM_KT_* class.
+struct Timer {
+    bool on = false;
+    std::vector<hipEvent_t> ev;   // pool, pairs (2i, 2i+1)
+    std::vector<int> cls;         // class of pair i since the last read
+    void begin(hipStream_t st) {
+        if (!on) return;
+        const size_t i = 2 * cls.size();
+        while (ev.size() < i + 2) {
+            hipEvent_t e = nullptr;
+            if (hipEventCreate(&e) != hipSuccess) { on = false; return; }
+            ev.push_back(e);
+        }
+        (void)hipEventRecord(ev[i], st);
+    }
+    void end(int c, hipStream_t st) {
+        if (!on) return;
+        (void)hipEventRecord(ev[2 * cls.size() + 1], st);
+        cls.push_back(c);
+    }
+    void release() { for (auto e : ev) (void)hipEventDestroy(e); ev.clear(); cls.clear(); }
+};
+
 struct Launch {
     OmSceneDev S;
     OmCamDev C;
@@ -35,6 +60,7 @@ struct Launch {
     bool count;
     int trace_mode;              // closest-hit kernel variant (om_render.hip MODE_*)
     uint32_t tail_bounce;        // first bounce run by the persistent tail kernel (0 = default)
+    Timer* timer;                // per-launch event timing (may be off)
 };
 
 // Renders P.sample_count samples of every listed pixel; returns 0 or a HIP error text.
