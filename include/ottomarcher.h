@@ -35,7 +35,7 @@
 extern "C" {
 #endif
 
-#define OM_ABI_VERSION 1
+#define OM_ABI_VERSION 2   /* 2: om-rng v2 path stream */
 
 typedef int32_t om_status;
 #define OM_OK 0
@@ -88,7 +88,7 @@ typedef struct om_render_params {
     float tmin, tmax;           /* 0.001 / 100.0 (main.rs:205-206) */
     uint32_t march_steps;       /* max march iterations (hits.rs:292 hard-codes 1024) */
     uint32_t adaptive;          /* 1 = retire pixels like Stats::add/ThreadPixels (render_thread.rs:31-38,97-101) */
-    uint64_t seed;              /* om-rng v1 seed (replaces thread_rng, utils.rs:25) */
+    uint64_t seed;              /* om-rng v2 path-stream seed (replaces thread_rng, utils.rs:25) */
 } om_render_params;
 
 /* Kernel choices (all produce bit-identical om_pixel_stats). */
@@ -162,7 +162,7 @@ om_status om_world_counts(const om_world* w, uint32_t counts[8]);
  * kind 7 torus -> 43 floats. */
 om_status om_world_export(const om_world* w, int32_t kind, uint32_t index, float* out, uint32_t out_floats);
 
-/* Front-end scene builders (main.rs:37-110) driven by om-rng v1 from `seed`.
+/* Front-end scene builders (main.rs:37-110) driven by om-rng's SplitMix64 from `seed`.
  * flags bit0: include the marched torus block (main.rs:73-81);
  * flags bit1: omit the parallelogram/triangle/cube blocks.
  * grid_half: 11 = random_scene's -11..11 grid; 50 = the 10k-sphere variant. */

@@ -148,6 +148,7 @@ struct OmSceneDev {
     const OmAlwaysRec* always2_rec;  // always2 with boxes (BVH2 traversal)
     uint32_t n_b2nodes, n_b2leaves;
     uint32_t b2_lds_bytes;        // node bytes when they fit the LDS budget, else 0 (global nodes)
+    uint32_t b2_stack;            // lane-stack entries the tree needs (its internal depth, <= 24)
 };
 
 struct OmCamDev {

@@ -307,7 +307,7 @@ namespace omd {
 // records (everything else is in always2).  Box tests only choose which exact tests
 // run (FMA allowed, conservative, see traced_sbvh); the acceptance keeps the
 // brute-force tie rule, so the winner is bit-identical to hits.rs:274-285.
-// A stack overflow (tree deeper than DEPTH) falls back to the reference loop.
+// The stack needs one entry per internal level (om_upload_world sizes it to the tree).
 // The reference loop's answer for a non-finite ray, in closed form (hits.rs:274-285):
 // every Sphere::hit accepts a NaN root (`disc < 0` and the range checks are all false
 // for NaN, traced.rs:46-55) and so does InfinitePlane::hit (traced.rs:108), while Cube
@@ -392,7 +392,7 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
             cur = stk[sp * STRIDE];
         }
     }
-    (void)overflow;  // unreachable: om_upload_world enables BVH2 only when depth <= DEPTH + 1
+    (void)overflow;  // unreachable: om_upload_world enables BVH2 only when depth <= DEPTH
     return best;
 }
 

@@ -48,8 +48,11 @@ namespace {
 constexpr uint32_t kNoSample = 0xFFFFFFFFu;
 enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL = 5, TR_BVH2_LDS = 6, TR_BVH2_GLOBAL = 7 };
 constexpr int kBlk = 256;                                         // workgroup = one queue segment
-constexpr int kStackDepth = 24;                                   // BVH2 per-lane LDS stack (u16 entries)
-constexpr uint32_t kStackBytes = kBlk * kStackDepth * 2u;         // 12 KiB per 256-lane workgroup
+constexpr int kStackDepth = 24;                                   // BVH2 per-lane LDS stack bound (u16 entries)
+// LDS bytes of the lane stack: S.b2_stack entries per lane (the tree's internal depth, 9 for
+// S-traced: 4.5 KiB per 256-lane workgroup instead of 12 KiB at the 24-entry bound, which
+// lifts the LDS-limited occupancy from 5 to 6 workgroups per CU).
+__host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) { return kBlk * S.b2_stack * 2u; }
 constexpr uint32_t kTailSpb = 4;                                  // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
 
@@ -147,7 +150,7 @@ __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every 
     if (TR == TR_BVH2_LDS) {
         const uint32_t nn = S.n_b2nodes * 4u;
         const uint4* sn = (const uint4*)S.b2nodes;
-        uint4* dst = wf_lds + kStackBytes / 16u;
+        uint4* dst = wf_lds + stack_bytes(S) / 16u;
         for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = sn[i];
         uint32_t* ldst = (uint32_t*)(dst + nn);
         for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += kBlk) ldst[i] = S.b2leaves[i];
@@ -462,7 +465,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
     int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
     if (tr == TR_BVH2_LDS) tr = L.S.n_b2nodes == 0 ? TR_BVH : (L.S.b2_lds_bytes ? TR_BVH2_LDS : TR_BVH2_GLOBAL);
-    const uint32_t lds = tr == TR_BVH2_LDS ? kStackBytes + L.S.b2_lds_bytes : tr == TR_BVH2_GLOBAL ? kStackBytes : 0u;
+    const uint32_t lds = tr == TR_BVH2_LDS ? stack_bytes(L.S) + L.S.b2_lds_bytes : tr == TR_BVH2_GLOBAL ? stack_bytes(L.S) : 0u;
     const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
     Gen R;
     R.C = L.C; R.jitter = L.jitter; R.stats = L.stats; R.pixels = L.pixels; R.n_pixels = n_px;

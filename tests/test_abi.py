@@ -36,7 +36,7 @@ def test_library_is_gfx950_code_object(om):
 
 def test_abi_version_and_struct_sizes(om):
     from raytracingoneweekend_amd import _lib
-    assert _lib.lib.om_abi_version() == 1
+    assert _lib.lib.om_abi_version() == 2
     assert C.sizeof(_lib.om_material) == 24
     assert C.sizeof(_lib.om_render_params) == 48
     assert _lib.PIXEL_STATS_DTYPE.itemsize == 40
