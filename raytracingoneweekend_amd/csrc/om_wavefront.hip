@@ -47,7 +47,22 @@ namespace {
 
 constexpr uint32_t kNoSample = 0xFFFFFFFFu;
 enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL = 5, TR_BVH2_LDS = 6, TR_BVH2_GLOBAL = 7 };
-constexpr int kBlk = 256;                                         // workgroup = one queue segment
+// Workgroup = one queue segment.  512 lanes share one LDS copy of the BVH2 nodes between 8
+// waves, so LDS stops capping occupancy, and 8 waves/SIMD (<= 64 VGPRs; bounce 0 spills
+// 8 B/lane) hide the incoherent bounces' latency.  Measured on C1 (tools/ablate.sh):
+// 256/no hint 3770, 256/8 3671, 512/- 3802, 512/8 3929, 1024/8 3368 Msamples/s.
+#ifndef OM_WF_BLOCK
+#define OM_WF_BLOCK 512
+#endif
+#ifndef OM_WF_WAVES
+#define OM_WF_WAVES 8
+#endif
+#if OM_WF_WAVES > 0                                               // occupancy request (waves per SIMD)
+#define OM_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(OM_WF_WAVES, OM_WF_WAVES)))
+#else
+#define OM_WAVES_ATTR
+#endif
+constexpr int kBlk = OM_WF_BLOCK;                                 // workgroup = one queue segment
 constexpr int kStackDepth = 24;                                   // BVH2 per-lane LDS stack bound (u16 entries)
 // LDS bytes of the lane stack: S.b2_stack entries per lane (the tree's internal depth, 9 for
 // S-traced: 4.5 KiB per 256-lane workgroup instead of 12 KiB at the 24-entry bound, which
@@ -225,7 +240,7 @@ __device__ __forceinline__ bool shade_path(const OmSceneDev& S, const OmParamsDe
 // Workgroup s: the paths of segment s of queue `in` (FIRST: the camera samples
 // [s*segcap, (s+1)*segcap) of the batch) -> survivors into segment s of `out`.
 template <int TR, bool COUNT, bool MARCH, bool FIRST>
-__global__ __launch_bounds__(kBlk) void k_bounce(OmSceneDev S, OmParamsDev P, Seg G, Gen R, Queue in,
+__global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmParamsDev P, Seg G, Gen R, Queue in,
                                                  const uint32_t* __restrict__ count_in, Queue out,
                                                  uint32_t* __restrict__ count_out, float4* __restrict__ res,
                                                  uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters) {
@@ -295,7 +310,7 @@ __global__ __launch_bounds__(kBlk) void k_bounce(OmSceneDev S, OmParamsDev P, Se
 // Workgroup b: every path of segments [b*kTailSpb, (b+1)*kTailSpb) of queue `in`, each
 // run to completion; a lane whose path ends takes the next one from an LDS counter.
 template <int TR, bool COUNT, bool MARCH>
-__global__ __launch_bounds__(kBlk) void k_tail(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
+__global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
                                                const uint32_t* __restrict__ count_in, float4* __restrict__ res,
                                                uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters) {
     __shared__ uint32_t pre[kTailSpb + 1];
@@ -457,8 +472,8 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint64_t max_paths = (uint64_t)n_px * batch;
-    // segments: ~16 workgroups per CU, a multiple of the tail grouping
-    uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * 16u);
+    // segments: ~4096 lanes per CU (16 workgroups of 256), a multiple of the tail grouping
+    uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (4096u / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
     const uint32_t segcap = (uint32_t)((max_paths + nseg - 1) / nseg);
     hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg);

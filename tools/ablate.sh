@@ -14,7 +14,21 @@ declare -A V=(
   [contract]="${COMMON/-ffp-contract=off/-ffp-contract=fast} $DEV"
   [rng32]="$COMMON $DEV -DOM_ABLATE_RNG"
   [ftz]="$COMMON --offload-arch=gfx950 -fhip-fp32-correctly-rounded-divide-sqrt -fgpu-flush-denormals-to-zero -fno-slp-vectorize"
+  # scheduling variants (bit-identical results): workgroup size x waves-per-SIMD request (0 = none)
+  [b256]="$COMMON $DEV -DOM_WF_BLOCK=256 -DOM_WF_WAVES=0"
+  [b256w8]="$COMMON $DEV -DOM_WF_BLOCK=256 -DOM_WF_WAVES=8"
+  [b512]="$COMMON $DEV -DOM_WF_BLOCK=512 -DOM_WF_WAVES=0"
+  [b1024w8]="$COMMON $DEV -DOM_WF_BLOCK=1024 -DOM_WF_WAVES=8"
 )
+if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
+if [ "$1" = resources ]; then
+  for k in ${VARIANTS:-${!V[@]}}; do
+    echo "== $k"; /opt/rocm/bin/hipcc ${V[$k]} -c -x hip $SRC/om_wavefront.hip -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | \
+      grep -E "Function Name|VGPRs:|ScratchSize|Occupancy" | sed -E 's/.*remark: +//; s/ \[-Rpass.*//' | paste - - - - | \
+      grep -E "k_(bounce|tail)ILi6ELb0ELb0" | awk '{print substr($3,1,40), $5, $8, $11}'
+  done
+  exit 0
+fi
 if [ "$1" = build ]; then
   mkdir -p _abl
   for k in "${!V[@]}"; do
