@@ -15,9 +15,10 @@ LIB_PATH = os.environ.get("OM_LIB") or os.path.join(_HERE, "libottomarcher.so")
 OM_OK = 0
 OM_ERR_INVALID, OM_ERR_DEVICE, OM_ERR_STATE, OM_ERR_UNSUPPORTED, OM_ERR_NOMEM = -1, -2, -3, -4, -5
 OM_LAMBERTIAN, OM_METAL, OM_DIELECTRIC = 0, 1, 2
-OM_KERNEL_AUTO, OM_KERNEL_BRUTE, OM_KERNEL_CULLED, OM_KERNEL_BVH, OM_KERNEL_SBVH, OM_KERNEL_BVH2 = 0, 1, 2, 3, 4, 5
+OM_KERNEL_AUTO, OM_KERNEL_BRUTE, OM_KERNEL_CULLED, OM_KERNEL_BVH, OM_KERNEL_SBVH, OM_KERNEL_BVH2, OM_KERNEL_BVH4 = \
+    0, 1, 2, 3, 4, 5, 6
 KERNELS = {"auto": OM_KERNEL_AUTO, "brute": OM_KERNEL_BRUTE, "culled": OM_KERNEL_CULLED, "bvh": OM_KERNEL_BVH,
-           "sbvh": OM_KERNEL_SBVH, "bvh2": OM_KERNEL_BVH2}
+           "sbvh": OM_KERNEL_SBVH, "bvh2": OM_KERNEL_BVH2, "bvh4": OM_KERNEL_BVH4}
 OM_PIPELINE_MEGAKERNEL, OM_PIPELINE_WAVEFRONT = 0, 1
 PIPELINES = {"megakernel": OM_PIPELINE_MEGAKERNEL, "wavefront": OM_PIPELINE_WAVEFRONT}
 

@@ -182,6 +182,8 @@ void build_bvh(const om_world& w, FrozenWorld& fw) {
 // cubes) re-emitted in depth-first order with a skip ("miss") link per node, and the
 // primitives' test records copied in leaf order so a leaf owns a contiguous run.
 // Everything else (planes, triangles, parallelograms, huge bounds) goes to always2.
+void build_bvh4(FrozenWorld& fw);
+
 void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     Builder b;
     std::vector<uint32_t> always;
@@ -302,6 +304,61 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
         for (uint32_t c : {fw.b2nodes[i].c0, fw.b2nodes[i].c1})
             if (!(c & OM_LEAF)) { depth[c] = depth[i] + 1; fw.b2_depth = std::max(fw.b2_depth, depth[c]); }
     }
+    build_bvh4(fw);
+}
+
+// BVH4: each wide node takes its BVH2 node's two children and keeps
+// replacing the internal child of largest surface area by that child's two children, up
+// to four.  Child boxes are the BVH2's (already conservative), so culling stays exact.
+void build_bvh4(FrozenWorld& fw) {
+    fw.b4nodes.clear();
+    fw.b4_depth = 0;
+    if (fw.b2nodes.empty()) return;
+    struct Ch { uint32_t code; float lo[3], hi[3]; };
+    auto kids = [&](uint32_t n, Ch* out) {
+        const OmBvh2Node& N = fw.b2nodes[n];
+        out[0].code = N.c0; out[1].code = N.c1;
+        for (int i = 0; i < 3; ++i) { out[0].lo[i] = N.lo0[i]; out[0].hi[i] = N.hi0[i]; out[1].lo[i] = N.lo1[i]; out[1].hi[i] = N.hi1[i]; }
+    };
+    auto area = [](const Ch& c) {
+        const double dx = std::max(0.0, (double)c.hi[0] - c.lo[0]), dy = std::max(0.0, (double)c.hi[1] - c.lo[1]),
+                     dz = std::max(0.0, (double)c.hi[2] - c.lo[2]);
+        return dx * dy + dy * dz + dz * dx;
+    };
+    struct Rec {
+        FrozenWorld& fw; decltype(kids)& kids; decltype(area)& area;
+        uint32_t go(uint32_t n2, uint32_t depth) {
+            std::vector<Ch> ch(2);
+            kids(n2, ch.data());
+            while (ch.size() < 4) {
+                int best = -1; double ba = -1.0;
+                for (size_t i = 0; i < ch.size(); ++i)
+                    if (!(ch[i].code & OM_LEAF) && area(ch[i]) > ba) { ba = area(ch[i]); best = (int)i; }
+                if (best < 0) break;
+                Ch two[2];
+                kids(ch[best].code, two);
+                ch[best] = two[0];
+                ch.insert(ch.begin() + best + 1, two[1]);
+            }
+            const uint32_t idx = (uint32_t)fw.b4nodes.size();
+            fw.b4nodes.push_back(OmBvh4Node{});
+            fw.b4_depth = std::max(fw.b4_depth, depth);
+            OmBvh4Node o{};
+            for (int k = 0; k < 4; ++k) {
+                if (k < (int)ch.size()) {
+                    o.lox[k] = ch[k].lo[0]; o.loy[k] = ch[k].lo[1]; o.loz[k] = ch[k].lo[2];
+                    o.hix[k] = ch[k].hi[0]; o.hiy[k] = ch[k].hi[1]; o.hiz[k] = ch[k].hi[2];
+                    o.child[k] = (uint16_t)((ch[k].code & OM_LEAF) ? ch[k].code : go(ch[k].code, depth + 1));
+                } else {
+                    o.lox[k] = o.loy[k] = o.loz[k] = o.hix[k] = o.hiy[k] = o.hiz[k] = 0.0f;
+                    o.child[k] = (uint16_t)OM_EMPTY;
+                }
+            }
+            fw.b4nodes[idx] = o;
+            return idx;
+        }
+    } r{fw, kids, area};
+    r.go(0, 1);
 }
 
 }  // namespace om

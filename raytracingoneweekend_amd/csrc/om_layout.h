@@ -97,6 +97,16 @@ struct OM_ALIGN16 OmSkipNode {
     uint32_t leaf;
 };
 
+// 4-wide BVH node (112 B), collapsed from the BVH2: up to four child boxes (SoA per
+// axis) and 16-bit child codes (node index | OM_LEAF + leaf index | OM_EMPTY).  Same
+// leaf table and records as the BVH2.
+#define OM_EMPTY 0xFFFFu
+struct OM_ALIGN16 OmBvh4Node {
+    float lox[4], loy[4], loz[4], hix[4], hiy[4], hiz[4];
+    uint16_t child[4];
+    uint32_t pad[2];
+};
+
 // Prim tested outside the BVH2 tree (always2), with a conservative box tested first:
 // inflated for triangles/parallelograms, infinite for planes and huge bounds.
 struct OM_ALIGN16 OmAlwaysRec {
@@ -149,6 +159,11 @@ struct OmSceneDev {
     uint32_t n_b2nodes, n_b2leaves;
     uint32_t b2_lds_bytes;        // node bytes when they fit the LDS budget, else 0 (global nodes)
     uint32_t b2_stack;            // lane-stack entries the tree needs (its internal depth, <= 24)
+    // BVH4 collapsed from the BVH2 (same leaf table / records / always2)
+    const OmBvh4Node* b4nodes;
+    uint32_t n_b4nodes;
+    uint32_t b4_lds_bytes;        // node bytes when they fit the LDS budget, else 0 (global nodes)
+    uint32_t b4_stack;            // lane-stack entries: 3 per level + 3 for the unconditional pushes
 };
 
 struct OmCamDev {

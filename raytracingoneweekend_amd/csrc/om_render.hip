@@ -386,7 +386,8 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         L.tail_bounce = c->tail_bounce;
         L.timer = &c->timer;
         L.trace_mode = mode == OM_KERNEL_BRUTE ? MODE_BRUTE : mode == OM_KERNEL_CULLED ? MODE_CULLED
-                     : mode == OM_KERNEL_BVH ? MODE_BVH : mode == OM_KERNEL_BVH2 ? 6 : MODE_SBVH_LDS;
+                     : mode == OM_KERNEL_BVH ? MODE_BVH : mode == OM_KERNEL_BVH2 ? 6
+                     : mode == OM_KERNEL_BVH4 ? 8 : MODE_SBVH_LDS;
         if (dev_pixels) {
             L.pixels = dev_pixels; L.n_pixels = n_pixels; L.stats_by_pixel = false;
         } else {
@@ -499,9 +500,8 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     S.n_snodes = (uint32_t)fw.snodes.size(); S.n_srecs = (uint32_t)fw.srecs.size(); S.n_always2 = (uint32_t)fw.always2.size();
     const size_t lds = fw.snodes.size() * sizeof(OmSkipNode) + fw.srecs.size() * sizeof(OmAffineTest);
     S.lds_bytes = lds <= kLdsBudget ? (uint32_t)(lds < 16 ? 16 : lds) : 0u;
-    // compressed BVH2: usable when its depth fits the 24-entry lane stack and node ids fit u16
-    // compressed BVH2: usable when node and leaf ids fit the 15-bit codes (a deeper
-    // tree than the lane stack falls back per ray to the reference loop)
+    // compressed BVH2: usable when node and leaf ids fit the 15-bit codes and its depth fits
+    // the lane-stack bound (otherwise the wavefront path uses the global-memory BVH)
     const bool b2_ok = !fw.b2nodes.empty() && fw.b2nodes.size() < 32768u && fw.b2leaves.size() < 32768u &&
                        fw.b2_depth <= 24u;   // lane stack bound (om_wavefront.hip kStackDepth)
     S.n_b2nodes = b2_ok ? (uint32_t)fw.b2nodes.size() : 0u;
@@ -509,6 +509,15 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     S.b2_stack = b2_ok ? fw.b2_depth : 0u;   // one push per internal level on the current path, deepest included
     const size_t b2_bytes = fw.b2nodes.size() * sizeof(OmBvh2Node) + fw.b2leaves.size() * 4u;
     S.b2_lds_bytes = (b2_ok && b2_bytes <= 40u * 1024u) ? (uint32_t)((b2_bytes + 15u) & ~(size_t)15u) : 0u;
+    // BVH4 (same leaf table): up to 3 pushes per level + 3 spare entries for the
+    // unconditional pushes, within the 48-entry bound of om_wavefront.hip
+    const uint32_t b4_stack = 3u * fw.b4_depth + 3u;
+    const bool b4_ok = b2_ok && !fw.b4nodes.empty() && fw.b4nodes.size() < 32768u && b4_stack <= 48u;
+    if (b4_ok && (s = upload(c, fw.b4nodes, &S.b4nodes)) != OM_OK) return s;
+    S.n_b4nodes = b4_ok ? (uint32_t)fw.b4nodes.size() : 0u;
+    S.b4_stack = b4_ok ? b4_stack : 0u;
+    const size_t b4_bytes = fw.b4nodes.size() * sizeof(OmBvh4Node) + fw.b2leaves.size() * 4u;
+    S.b4_lds_bytes = (b4_ok && b4_bytes <= 40u * 1024u) ? (uint32_t)((b4_bytes + 15u) & ~(size_t)15u) : 0u;
     OM_HIP(c, hipStreamSynchronize(c->stream));
     c->have_world = true;
     return OM_OK;
@@ -516,7 +525,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
 
 om_status om_set_kernel(om_ctx* c, int32_t k) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
-    if (k < OM_KERNEL_AUTO || k > OM_KERNEL_BVH2) return set_err(c, OM_ERR_INVALID, "om_set_kernel: unknown kernel");
+    if (k < OM_KERNEL_AUTO || k > OM_KERNEL_BVH4) return set_err(c, OM_ERR_INVALID, "om_set_kernel: unknown kernel");
     c->kernel = k;
     return OM_OK;
 }

@@ -128,6 +128,42 @@ __device__ __forceinline__ int traced_bvh(const OmSceneDev& S, F3 o, F3 d, float
     return best;
 }
 
+// The primitives outside the BVH trees (always2): conservative box first, then the
+// exact test with the brute-force tie rule.
+template <class Wk>
+__device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, float tmin, float ix, float iy, float iz,
+                                              float nox, float noy, float noz, float t_lo, float& closest, int& best, Wk& w) {
+    for (uint32_t k = 0; k < S.n_always2; ++k) {
+        const OmAlwaysRec A = S.always2_rec[k];
+        w.add_pre();
+        const float t_hi = closest * 1.0001f + 1e-3f;
+        const float x0 = __builtin_fmaf(A.lo[0], ix, nox), x1 = __builtin_fmaf(A.hi[0], ix, nox);
+        const float y0 = __builtin_fmaf(A.lo[1], iy, noy), y1 = __builtin_fmaf(A.hi[1], iy, noy);
+        const float z0 = __builtin_fmaf(A.lo[2], iz, noz), z1 = __builtin_fmaf(A.hi[2], iz, noz);
+        const float n0 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+        const float f0 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        if (!(n0 > f0)) offer(S, A.gi, o, d, tmin, closest, best, w);
+    }
+}
+
+// Leaf of the BVH2/BVH4: its Sphere/Cube records, tested in place (tag bit 31 = cube).
+template <class Wk>
+__device__ __forceinline__ void test_leaf(const OmAffineTest* recs, uint32_t lf, F3 o, F3 d, float tmin, float& closest,
+                                          int& best, Wk& w) {
+    const uint32_t first = lf >> 8, cnt = lf & 255u;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const OmAffineTest R = recs[first + k];
+        uint32_t tag;
+        __builtin_memcpy(&tag, &R.pad, 4);
+        const uint32_t gi = tag & 0x7FFFFFFFu;
+        float t;
+        int ax;
+        w.add_prim();
+        const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root(R, o, d, tmin, closest, t);
+        if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
+    }
+}
+
 // Stackless BVH traversal.  Nodes are visited in depth-first
 // order: box hit -> next node (internal) or the leaf's records then `skip`; miss ->
 // `skip`.  No per-lane stack (no scratch), one 32-B node read per step.  The box test
@@ -145,17 +181,7 @@ __device__ __forceinline__ int traced_sbvh(const OmSceneDev& S, const OmSkipNode
     const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
-    for (uint32_t k = 0; k < S.n_always2; ++k) {      // box first, then the exact test
-        const OmAlwaysRec A = S.always2_rec[k];
-        w.add_pre();
-        const float t_hi = closest * 1.0001f + 1e-3f;
-        const float x0 = __builtin_fmaf(A.lo[0], ix, nox), x1 = __builtin_fmaf(A.hi[0], ix, nox);
-        const float y0 = __builtin_fmaf(A.lo[1], iy, noy), y1 = __builtin_fmaf(A.hi[1], iy, noy);
-        const float z0 = __builtin_fmaf(A.lo[2], iz, noz), z1 = __builtin_fmaf(A.hi[2], iz, noz);
-        const float n0 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-        const float f0 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
-        if (!(n0 > f0)) offer(S, A.gi, o, d, tmin, closest, best, w);
-    }
+    offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
     const uint32_t n = S.n_snodes;
     uint32_t node = 0;
     while (node < n) {
@@ -329,36 +355,14 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
     const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
-    for (uint32_t k = 0; k < S.n_always2; ++k) {      // box first, then the exact test
-        const OmAlwaysRec A = S.always2_rec[k];
-        w.add_pre();
-        const float t_hi = closest * 1.0001f + 1e-3f;
-        const float x0 = __builtin_fmaf(A.lo[0], ix, nox), x1 = __builtin_fmaf(A.hi[0], ix, nox);
-        const float y0 = __builtin_fmaf(A.lo[1], iy, noy), y1 = __builtin_fmaf(A.hi[1], iy, noy);
-        const float z0 = __builtin_fmaf(A.lo[2], iz, noz), z1 = __builtin_fmaf(A.hi[2], iz, noz);
-        const float n0 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-        const float f0 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
-        if (!(n0 > f0)) offer(S, A.gi, o, d, tmin, closest, best, w);
-    }
+    offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
     const OmAffineTest* recs = S.srecs;
     uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
     int sp = 0;
     bool overflow = false;
     for (;;) {
         if (cur & OM_LEAF) {                            // the single leaf site
-            const uint32_t lf = leaves[cur & (OM_LEAF - 1u)];
-            const uint32_t first = lf >> 8, cnt = lf & 255u;
-            for (uint32_t k = 0; k < cnt; ++k) {
-                const OmAffineTest R = recs[first + k];
-                uint32_t tag;
-                __builtin_memcpy(&tag, &R.pad, 4);
-                const uint32_t gi = tag & 0x7FFFFFFFu;
-                float t;
-                int ax;
-                w.add_prim();
-                const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root(R, o, d, tmin, closest, t);
-                if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
-            }
+            test_leaf(recs, leaves[cur & (OM_LEAF - 1u)], o, d, tmin, closest, best, w);
             if (sp == 0) break;
             --sp;
             cur = stk[sp * STRIDE];
@@ -393,6 +397,80 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
         }
     }
     (void)overflow;  // unreachable: om_upload_world enables BVH2 only when depth <= DEPTH
+    return best;
+}
+
+
+// 4-wide BVH traversal: one 112-B node read gives four slab tests; the
+// hit children are ordered near-first by a 5-compare sorting network, the nearest is
+// visited next and the others go on the lane's LDS stack with three unconditional u16
+// writes (no divergent push branches; the stack holds 3 spare entries for them).
+template <int STRIDE, class Wk>
+__device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node* nodes, const uint32_t* leaves, uint16_t* stk,
+                                           F3 o, F3 d, float tmin, float& closest, Wk& w) {
+    if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
+    int best = -1;
+    const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
+    const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
+    const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
+    const float t_lo = tmin * 0.5f - 1e-3f;
+    offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
+    const OmAffineTest* recs = S.srecs;
+    uint32_t cur = 0;
+    int sp = 0;
+    for (;;) {
+        if (cur & OM_LEAF) {
+            test_leaf(recs, leaves[cur & (OM_LEAF - 1u)], o, d, tmin, closest, best, w);
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * STRIDE];
+            continue;
+        }
+        const OmBvh4Node& N = nodes[cur];
+        w.add_pre(4);
+        const float t_hi = closest * 1.0001f + 1e-3f;
+        float key[4];
+        uint32_t code[4];
+        int n = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float x0 = __builtin_fmaf(N.lox[k], ix, nox), x1 = __builtin_fmaf(N.hix[k], ix, nox);
+            const float y0 = __builtin_fmaf(N.loy[k], iy, noy), y1 = __builtin_fmaf(N.hiy[k], iy, noy);
+            const float z0 = __builtin_fmaf(N.loz[k], iz, noz), z1 = __builtin_fmaf(N.hiz[k], iz, noz);
+            const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
+            const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+            const uint32_t c = N.child[k];
+            const bool h = !(tn > tf) && c != OM_EMPTY;
+            key[k] = h ? tn : INFINITY;
+            code[k] = c;
+            n += h ? 1 : 0;
+        }
+        if (n == 0) {
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * STRIDE];
+            continue;
+        }
+#define OM_CAS(a, b)                                                                          \
+        {                                                                                     \
+            const bool sw = key[b] < key[a];                                                  \
+            const float ka = key[a], kb = key[b];                                             \
+            const uint32_t ca = code[a], cb = code[b];                                        \
+            key[a] = sw ? kb : ka; key[b] = sw ? ka : kb;                                     \
+            code[a] = sw ? cb : ca; code[b] = sw ? ca : cb;                                   \
+        }
+        OM_CAS(0, 1) OM_CAS(2, 3) OM_CAS(0, 2) OM_CAS(1, 3) OM_CAS(1, 2)
+#undef OM_CAS
+        // stack, bottom -> top: the n-1 far children, farthest first (nearest popped first)
+        const uint32_t w0 = n == 4 ? code[3] : (n == 3 ? code[2] : code[1]);
+        const uint32_t w1 = n == 4 ? code[2] : code[1];
+        stk[sp * STRIDE] = (uint16_t)w0;
+        stk[(sp + 1) * STRIDE] = (uint16_t)w1;
+        stk[(sp + 2) * STRIDE] = (uint16_t)code[1];
+        sp += n - 1;
+        cur = code[0];
+    }
     return best;
 }
 

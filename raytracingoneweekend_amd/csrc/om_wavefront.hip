@@ -46,7 +46,8 @@ void Buffers::release() {
 namespace {
 
 constexpr uint32_t kNoSample = 0xFFFFFFFFu;
-enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL = 5, TR_BVH2_LDS = 6, TR_BVH2_GLOBAL = 7 };
+enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL = 5, TR_BVH2_LDS = 6, TR_BVH2_GLOBAL = 7,
+       TR_BVH4_LDS = 8, TR_BVH4_GLOBAL = 9 };
 // Workgroup = one queue segment.  512 lanes share one LDS copy of the BVH2 nodes between 8
 // waves, so LDS stops capping occupancy, and 8 waves/SIMD (<= 64 VGPRs; bounce 0 spills
 // 8 B/lane) hide the incoherent bounces' latency.  Measured on C1 (tools/ablate.sh):
@@ -67,7 +68,10 @@ constexpr int kStackDepth = 24;                                   // BVH2 per-la
 // LDS bytes of the lane stack: S.b2_stack entries per lane (the tree's internal depth, 9 for
 // S-traced: 4.5 KiB per 256-lane workgroup instead of 12 KiB at the 24-entry bound, which
 // lifts the LDS-limited occupancy from 5 to 6 workgroups per CU).
-__host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) { return kBlk * S.b2_stack * 2u; }
+template <int TR>
+__host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
+    return kBlk * ((TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) ? S.b4_stack : S.b2_stack) * 2u;
+}
 constexpr uint32_t kTailSpb = 4;                                  // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
 
@@ -149,11 +153,12 @@ __device__ __forceinline__ void store_path(const Queue& Q, uint64_t i, const Pat
     Q.qr[i] = make_uint4(p.g.s, p.g.k, p.slot, 0u);
 }
 
-// Scene data a workgroup traces against: BVH2 nodes + leaf table staged in LDS behind
+// Scene data a workgroup traces against: BVH2/BVH4 nodes + leaf table staged in LDS behind
 // the per-lane stack ([stack][nodes][leaf table]), or read through L2.
 struct Tracer {
     const OmBvh2Node* b2n;
-    const uint32_t* b2l;
+    const OmBvh4Node* b4n;
+    const uint32_t* bl;
     uint16_t* stk;
 };
 
@@ -161,16 +166,16 @@ template <int TR>
 __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every thread of the block calls it
     Tracer t;
     t.stk = (uint16_t*)wf_lds + threadIdx.x;
-    t.b2n = S.b2nodes; t.b2l = S.b2leaves;
-    if (TR == TR_BVH2_LDS) {
-        const uint32_t nn = S.n_b2nodes * 4u;
-        const uint4* sn = (const uint4*)S.b2nodes;
-        uint4* dst = wf_lds + stack_bytes(S) / 16u;
+    t.b2n = S.b2nodes; t.b4n = S.b4nodes; t.bl = S.b2leaves;
+    if (TR == TR_BVH2_LDS || TR == TR_BVH4_LDS) {
+        const uint32_t nn = TR == TR_BVH2_LDS ? S.n_b2nodes * 4u : S.n_b4nodes * 7u;   // uint4 per node
+        const uint4* sn = TR == TR_BVH2_LDS ? (const uint4*)S.b2nodes : (const uint4*)S.b4nodes;
+        uint4* dst = wf_lds + stack_bytes<TR>(S) / 16u;
         for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = sn[i];
         uint32_t* ldst = (uint32_t*)(dst + nn);
         for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += kBlk) ldst[i] = S.b2leaves[i];
         __syncthreads();
-        t.b2n = (const OmBvh2Node*)dst; t.b2l = ldst;
+        t.b2n = (const OmBvh2Node*)dst; t.b4n = (const OmBvh4Node*)dst; t.bl = ldst;
     }
     return t;
 }
@@ -183,7 +188,8 @@ __device__ __forceinline__ int trace(const OmSceneDev& S, const OmParamsDev& P, 
                                      float& closest, Wk& w) {
     closest = P.tmax;
     int best;
-    if (TR == TR_BVH2_LDS || TR == TR_BVH2_GLOBAL) best = traced_bvh2<kStackDepth, kBlk>(S, T.b2n, T.b2l, T.stk, o, d, P.tmin, closest, w);
+    if (TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) best = traced_bvh4<kBlk>(S, T.b4n, T.bl, T.stk, o, d, P.tmin, closest, w);
+    else if (TR == TR_BVH2_LDS || TR == TR_BVH2_GLOBAL) best = traced_bvh2<kStackDepth, kBlk>(S, T.b2n, T.bl, T.stk, o, d, P.tmin, closest, w);
     else if (TR == TR_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
     else if (TR == TR_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
     else best = traced_brute<TR == TR_CULLED>(S, o, d, P.tmin, closest, w);
@@ -479,8 +485,12 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg);
     if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
     int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
+    if (tr == TR_BVH4_LDS) tr = L.S.n_b4nodes == 0 ? TR_BVH2_LDS : (L.S.b4_lds_bytes ? TR_BVH4_LDS : TR_BVH4_GLOBAL);
     if (tr == TR_BVH2_LDS) tr = L.S.n_b2nodes == 0 ? TR_BVH : (L.S.b2_lds_bytes ? TR_BVH2_LDS : TR_BVH2_GLOBAL);
-    const uint32_t lds = tr == TR_BVH2_LDS ? stack_bytes(L.S) + L.S.b2_lds_bytes : tr == TR_BVH2_GLOBAL ? stack_bytes(L.S) : 0u;
+    const uint32_t lds = tr == TR_BVH2_LDS ? stack_bytes<TR_BVH2_LDS>(L.S) + L.S.b2_lds_bytes
+                       : tr == TR_BVH2_GLOBAL ? stack_bytes<TR_BVH2_GLOBAL>(L.S)
+                       : tr == TR_BVH4_LDS ? stack_bytes<TR_BVH4_LDS>(L.S) + L.S.b4_lds_bytes
+                       : tr == TR_BVH4_GLOBAL ? stack_bytes<TR_BVH4_GLOBAL>(L.S) : 0u;
     const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
     Gen R;
     R.C = L.C; R.jitter = L.jitter; R.stats = L.stats; R.pixels = L.pixels; R.n_pixels = n_px;
@@ -498,6 +508,8 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
             case TR_BVH: run_tr<TR_BVH>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
             case TR_SBVH_GLOBAL: run_tr<TR_SBVH_GLOBAL>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
             case TR_BVH2_LDS: run_tr<TR_BVH2_LDS>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
+            case TR_BVH4_LDS: run_tr<TR_BVH4_LDS>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
+            case TR_BVH4_GLOBAL: run_tr<TR_BVH4_GLOBAL>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
             default: run_tr<TR_BVH2_GLOBAL>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
         }
         const uint32_t grid_a = (n_px + kBlk - 1) / kBlk;

@@ -22,7 +22,7 @@ STRUCTS = {
     "om_pixel_stats": ["bloom", "sum", "n", "avg_depth", "bad_avgs", "color", "flags", "reserved"],
 }
 ENUMS = ["OM_LAMBERTIAN", "OM_METAL", "OM_DIELECTRIC", "OM_KERNEL_AUTO", "OM_KERNEL_BRUTE", "OM_KERNEL_CULLED",
-         "OM_KERNEL_BVH", "OM_KERNEL_SBVH", "OM_KERNEL_BVH2", "OM_PIPELINE_MEGAKERNEL", "OM_PIPELINE_WAVEFRONT",
+         "OM_KERNEL_BVH", "OM_KERNEL_SBVH", "OM_KERNEL_BVH2", "OM_KERNEL_BVH4", "OM_PIPELINE_MEGAKERNEL", "OM_PIPELINE_WAVEFRONT",
          "OM_KT_BOUNCE0", "OM_KT_BOUNCE", "OM_KT_TAIL", "OM_KT_ACCUMULATE", "OM_KT_MEGAKERNEL", "OM_KT_N",
          "OM_OK", "OM_ERR_INVALID", "OM_ERR_DEVICE", "OM_ERR_STATE", "OM_ERR_UNSUPPORTED", "OM_ERR_NOMEM",
          "OM_ABI_VERSION"]
@@ -79,7 +79,8 @@ def test_enum_values_match_binding(om, c_layout):
         assert c_layout[f"OM_KT_{k.upper()}"] == i
     assert c_layout["OM_KT_N"] == len(_lib.KT_CLASSES)
     kernels = {"auto": "OM_KERNEL_AUTO", "brute": "OM_KERNEL_BRUTE", "culled": "OM_KERNEL_CULLED",
-               "bvh": "OM_KERNEL_BVH", "sbvh": "OM_KERNEL_SBVH", "bvh2": "OM_KERNEL_BVH2"}
+               "bvh": "OM_KERNEL_BVH", "sbvh": "OM_KERNEL_SBVH", "bvh2": "OM_KERNEL_BVH2",
+               "bvh4": "OM_KERNEL_BVH4"}
     for name, const in kernels.items():
         assert _lib.KERNELS[name] == c_layout[const], name
     assert _lib.PIPELINES["megakernel"] == c_layout["OM_PIPELINE_MEGAKERNEL"]

@@ -54,7 +54,7 @@ def _gpu_render(om, world, cam, W, H, spp, seed, kernel, march_steps=1024):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["brute", "culled", "bvh", "sbvh", "bvh2"])
+@pytest.mark.parametrize("kernel", ["brute", "culled", "bvh", "sbvh", "bvh2", "bvh4"])
 def test_gpu_matches_golden_images(om, oracle, kernel):
     W, H = 40, 24
     assert np.array_equal(_gpu_render(om, om.random_scene(0x5EED), om.default_camera(W / H), W, H, 8, 3, kernel),

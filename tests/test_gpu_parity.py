@@ -8,7 +8,7 @@ from scenes_common import compare_stats, kitchen_sink
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["brute", "culled", "bvh", "sbvh", "bvh2"]
+KERNELS = ["brute", "culled", "bvh", "sbvh", "bvh2", "bvh4"]
 PIPELINES = ["megakernel", "wavefront"]
 COMBOS = [(k, p) for p in PIPELINES for k in KERNELS]
 
@@ -104,7 +104,7 @@ def test_shallow_depth_and_exhaustion(om, oracle, pipeline):
 
 
 @pytest.mark.parametrize("kernel", [("bvh", "megakernel"), ("sbvh", "megakernel"), ("bvh", "wavefront"),
-                                    ("sbvh", "wavefront"), ("bvh2", "wavefront")])
+                                    ("sbvh", "wavefront"), ("bvh2", "wavefront"), ("bvh4", "wavefront")])
 def test_ten_k_scene_bvh_bit_exact(om, oracle, kernel):
     W, H, SPP = 32, 18, 2
     got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED, grid_half=50, extras=False),
