@@ -346,7 +346,8 @@ __device__ __forceinline__ int nonfinite_hit(const OmSceneDev& S, float& closest
 }
 
 template <int DEPTH, int STRIDE, class Wk>
-__device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node* nodes, const uint32_t* leaves, uint16_t* stk,
+__device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node* nodes, const uint32_t* leaves,
+                                           const OmAffineTest* recs, uint16_t* stk,
                                            F3 o, F3 d, float tmin, float& closest, Wk& w) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
@@ -356,7 +357,6 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
-    const OmAffineTest* recs = S.srecs;
     uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
     int sp = 0;
     bool overflow = false;
@@ -406,7 +406,8 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
 // visited next and the others go on the lane's LDS stack with three unconditional u16
 // writes (no divergent push branches; the stack holds 3 spare entries for them).
 template <int STRIDE, class Wk>
-__device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node* nodes, const uint32_t* leaves, uint16_t* stk,
+__device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node* nodes, const uint32_t* leaves,
+                                           const OmAffineTest* recs, uint16_t* stk,
                                            F3 o, F3 d, float tmin, float& closest, Wk& w) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
@@ -416,7 +417,6 @@ __device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
-    const OmAffineTest* recs = S.srecs;
     uint32_t cur = 0;
     int sp = 0;
     for (;;) {

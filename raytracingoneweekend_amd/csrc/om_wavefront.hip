@@ -159,6 +159,7 @@ struct Tracer {
     const OmBvh2Node* b2n;
     const OmBvh4Node* b4n;
     const uint32_t* bl;
+    const OmAffineTest* recs;
     uint16_t* stk;
 };
 
@@ -166,7 +167,7 @@ template <int TR>
 __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every thread of the block calls it
     Tracer t;
     t.stk = (uint16_t*)wf_lds + threadIdx.x;
-    t.b2n = S.b2nodes; t.b4n = S.b4nodes; t.bl = S.b2leaves;
+    t.b2n = S.b2nodes; t.b4n = S.b4nodes; t.bl = S.b2leaves; t.recs = S.srecs;
     if (TR == TR_BVH2_LDS || TR == TR_BVH4_LDS) {
         const uint32_t nn = TR == TR_BVH2_LDS ? S.n_b2nodes * 4u : S.n_b4nodes * 7u;   // uint4 per node
         const uint4* sn = TR == TR_BVH2_LDS ? (const uint4*)S.b2nodes : (const uint4*)S.b4nodes;
@@ -188,8 +189,8 @@ __device__ __forceinline__ int trace(const OmSceneDev& S, const OmParamsDev& P, 
                                      float& closest, Wk& w) {
     closest = P.tmax;
     int best;
-    if (TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) best = traced_bvh4<kBlk>(S, T.b4n, T.bl, T.stk, o, d, P.tmin, closest, w);
-    else if (TR == TR_BVH2_LDS || TR == TR_BVH2_GLOBAL) best = traced_bvh2<kStackDepth, kBlk>(S, T.b2n, T.bl, T.stk, o, d, P.tmin, closest, w);
+    if (TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) best = traced_bvh4<kBlk>(S, T.b4n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
+    else if (TR == TR_BVH2_LDS || TR == TR_BVH2_GLOBAL) best = traced_bvh2<kStackDepth, kBlk>(S, T.b2n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
     else if (TR == TR_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
     else if (TR == TR_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
     else best = traced_brute<TR == TR_CULLED>(S, o, d, P.tmin, closest, w);
@@ -293,7 +294,23 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
             if (live) {
                 float closest;
                 const int best = trace<TR, MARCH>(S, P, T, p.o, p.d, closest, w);
+#ifdef OM_ABLATE_TRACE2X   // timing ablation (tools/ablate.sh): the trace runs twice, same answer
+                {
+                    F3 o2 = p.o;
+                    o2.x += P.march_steps == 0xDEADBEEFu ? 1.0f : 0.0f;
+                    float c2;
+                    const int b2 = trace<TR, MARCH>(S, P, T, o2, p.d, c2, w);
+                    if (b2 != best || c2 != closest) res_id[0] = 0xDEADu;
+                }
+#endif
                 if (!FIRST) load_rest(in, i, p);
+#ifdef OM_ABLATE_SHADE2X   // timing ablation: shade a copy first (same result slot, same values)
+                {
+                    Path p2 = p;
+                    p2.cur.x *= P.march_steps == 0xDEADBEEFu ? 2.0f : 1.0f;
+                    if (shade_path(S, P, depth_cap, p2, closest, best, res, res_id) && p2.seg == 0xFFFFFFu) res_id[1] = 0u;
+                }
+#endif
                 keep = shade_path(S, P, depth_cap, p, closest, best, res, res_id);
                 if (COUNT) segs++;
             }

@@ -19,6 +19,9 @@ declare -A V=(
   [b256w8]="$COMMON $DEV -DOM_WF_BLOCK=256 -DOM_WF_WAVES=8"
   [b512]="$COMMON $DEV -DOM_WF_BLOCK=512 -DOM_WF_WAVES=0"
   [b1024w8]="$COMMON $DEV -DOM_WF_BLOCK=1024 -DOM_WF_WAVES=8"
+  # cost split of the fused bounce kernel: run one half twice
+  [trace2x]="$COMMON $DEV -DOM_ABLATE_TRACE2X"
+  [shade2x]="$COMMON $DEV -DOM_ABLATE_SHADE2X"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
