@@ -34,6 +34,21 @@ from raytracingoneweekend_amd import shard  # noqa: E402
 
 W, H, MAX_DEPTH, TMIN, TMAX, SEED, SCENE_SEED = 1920, 1080, 50, 0.001, 100.0, 1, 0x5EED
 SPP_PER_STEP = 16
+# BASELINE.json configs: C1 is the metric's workload (the default line); C2/C3 are measured
+# with --config for DESIGN.md (the marched SDF scene at 256 march steps, the 10k-sphere BVH).
+CONFIGS = {
+    "C1": {"scene": "S-traced", "spp": 512, "march_steps": 1024},
+    "C2": {"scene": "S-marched", "spp": 256, "march_steps": 256},
+    "C3": {"scene": "S-10k", "spp": 256, "march_steps": 1024},
+}
+
+
+def make_scene(name, om_or_oracle):
+    if name == "S-traced":
+        return om_or_oracle.random_scene(SCENE_SEED)
+    if name == "S-marched":
+        return om_or_oracle.marched_scene()
+    return om_or_oracle.random_scene(SCENE_SEED, grid_half=50, extras=False)
 PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md; FMA = 2 flop)
 PEAK_HBM_GBS = 8000.0
 
@@ -53,40 +68,48 @@ BOUNCE_FAMILY = ("bounce0", "bounce", "tail")            # one fused trace+shade
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 
-def cpu_baseline(budget_s=12.0):
+def cpu_baseline(budget_s=12.0, cfg="C1"):
     """Oracle (CPU restatement, `port`) on the host: the reference's thread scheme
-    (num_cpus-1 workers, 2730-px round-robin chunks, main.rs:170-189) on the same C1 frame."""
+    (num_cpus-1 workers, 2730-px round-robin chunks, main.rs:170-189) on the same frame."""
     from oracle import oracle as O  # checker / baseline only
     cores = max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 2)) - 1)
-    ow = O.random_scene(SCENE_SEED)
-    cam = O.default_camera(W / H)
+    ow = make_scene(CONFIGS[cfg]["scene"], O)
+    # the oracle is brute force: for the 10k-sphere scene a 1/64-area frame of the same
+    # scene and camera (per-sample cost does not depend on the resolution)
+    w, h = (W // 8, H // 8) if cfg == "C3" else (W, H)
+    cam = O.default_camera(w / h)
     done, t_total, passes = 0, 0.0, 0
-    stats = np.zeros(W * H, dtype=O.PIXEL_STATS_DTYPE)
+    stats = np.zeros(w * h, dtype=O.PIXEL_STATS_DTYPE)
     spp_total = 64
     while passes == 0 or (t_total < budget_s and passes < spp_total):
-        p = O.params(W, H, spp_total, sample_count=1, max_depth=MAX_DEPTH, seed=SEED)
+        p = O.params(w, h, spp_total, sample_count=1, max_depth=MAX_DEPTH, seed=SEED,
+                     march_steps=CONFIGS[cfg]["march_steps"])
         t0 = time.perf_counter()
         _, ctr = O.render(ow, cam, p, stats=stats, nthreads=cores)
         t_total += time.perf_counter() - t0
         done += ctr["samples"]
         passes += 1
     return {"value": done / t_total / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
-            "sample": f"C1 frame {W}x{H}, {passes} spp (full passes), depth {MAX_DEPTH}, S-traced, "
+            "sample": f"{cfg} frame {w}x{h}, {passes} spp (full passes), depth {MAX_DEPTH}, {CONFIGS[cfg]['scene']}, "
                       f"{cores} threads, {t_total:.1f} s"}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--config", default="C1", choices=list(CONFIGS))
+    ap.add_argument("--steps", type=int, default=None, help="default: the config's spp / 16 (C1: 32)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
-    ap.add_argument("--pipeline", default="wavefront", choices=list(L.PIPELINES))
+    ap.add_argument("--pipeline", default="auto", choices=list(L.PIPELINES))
     ap.add_argument("--tail", type=int, default=0, help="first bounce of the persistent tail launch (0 = library default)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no per-launch HIP events in the timed region")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    if args.steps is None:
+        args.steps = cfg["spp"] // SPP_PER_STEP
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -103,7 +126,7 @@ def main():
     torch.cuda.set_stream(stream)
     sptr = C.c_void_p(stream.cuda_stream)
     assert sptr.value, "need a non-default stream handle"
-    world = om.random_scene(SCENE_SEED)
+    world = make_scene(cfg["scene"], om)
     cam = om.default_camera(W / H)
     frozen = world.freeze(cam, device=local_rank, kernel=args.kernel, pipeline=args.pipeline)
     ctx = frozen.ctx
@@ -119,7 +142,8 @@ def main():
         L.check(L.lib.om_render_device_pixels(ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(stats.data_ptr()),
                                               C.c_void_p(dev_pix.data_ptr()), n_px, sptr), ctx)
 
-    p = om.make_params(MAX_DEPTH, TMIN, TMAX, spp_total, W, H, sample_count=spp_step, seed=SEED)
+    p = om.make_params(MAX_DEPTH, TMIN, TMAX, spp_total, W, H, sample_count=spp_step, seed=SEED,
+                       march_steps=cfg["march_steps"])
     for _ in range(args.warmup):
         step(p)
     torch.cuda.synchronize()
@@ -182,9 +206,8 @@ def main():
 
     # roofline of the dominant kernel: the fused trace+shade bounce kernel (all its launches:
     # bounce 0, bounces 1.., tail), algorithmic flops from the live counters / its event time
-    fam = [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
-    if args.pipeline == "megakernel":
-        fam = [L.KT_CLASSES.index("megakernel")]
+    mega = kt.launches[L.KT_CLASSES.index("megakernel")] > 0     # the pipeline that actually ran (auto)
+    fam = [L.KT_CLASSES.index("megakernel")] if mega else [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
     launches = sum(kt.launches[i] for i in fam)
     kern_s = sum(kt.ms[i] for i in fam) / 1e3
     roof = None
@@ -195,12 +218,12 @@ def main():
         avg_launch_s = kern_s / launches
         achieved_tflops = flops / kern_s / 1e12
         traffic, traffic_src = None, None
-        if os.path.exists(PMC_TRAFFIC) and args.pipeline == "wavefront" and args.kernel == "auto":
+        if os.path.exists(PMC_TRAFFIC) and not mega and args.kernel == "auto" and args.config == "C1":
             pm = json.load(open(PMC_TRAFFIC))
             traffic, traffic_src = pm["hbm_bytes_per_launch"], pm["source"]
         roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": traffic,
-                "kernel": "k_bounce0+k_bounce+k_tail (fused trace+shade)" if args.pipeline == "wavefront" else "render_kernel",
+                "kernel": "render_kernel (megakernel)" if mega else "k_bounce0+k_bounce+k_tail (fused trace+shade)",
                 "launches_per_step": round(launches / args.steps, 2), "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "flop_per_launch": round(flops / launches), "algorithmic_bytes_per_launch": round(nbytes / launches),
                 "hbm_achieved_gbs": round(nbytes / kern_s / 1e9, 2), "traffic_source": traffic_src,
@@ -215,7 +238,7 @@ def main():
             assert int(frame["n"].min()) == spp_total, "gathered frame incomplete"
         cpu = None
         if world_size == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_budget)
+            cpu = cpu_baseline(args.cpu_budget, args.config)
         out = {
             "metric": "Msamples/s (W×H×spp/s) + achieved HBM GB/s, 1080p@512spp traced scene",
             "value": round(value, 3),
@@ -228,10 +251,12 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic: S-traced random_scene (om-rng seed 0x5EED), render seed 1",
-            "config": {"workload": f"C1 S-traced {W}x{H}, {spp_total} spp timed ({spp_step} spp/step), depth {MAX_DEPTH}",
+            "data": f"synthetic: {cfg['scene']} (om-rng scene seed 0x5EED), render seed 1",
+            "config": {"workload": f"{args.config} {cfg['scene']} {W}x{H}, {spp_total} spp timed ({spp_step} spp/step), "
+                                   f"depth {MAX_DEPTH}" + (f", {cfg['march_steps']} march steps" if args.config == "C2" else ""),
                        "width": W, "height": H, "spp_per_step": spp_step, "max_depth": MAX_DEPTH,
-                       "parallelism": f"tile{world_size}", "kernel": args.kernel, "pipeline": args.pipeline,
+                       "parallelism": f"tile{world_size}", "kernel": args.kernel,
+                       "pipeline": args.pipeline + (("->megakernel" if mega else "->wavefront") if args.pipeline == "auto" else ""),
                        "tail_bounce": args.tail or "default"},
             "hbm_gbs": hbm_gbs,
             "roofline": roof,

@@ -201,12 +201,14 @@ om_status om_reset_counters(om_ctx* ctx, void* stream);
 /* Work counting on (default) / off.  Off selects kernel builds with the counters
  * compiled out (fewer registers); results are bit-identical either way. */
 om_status om_set_counting(om_ctx* ctx, int32_t enable);
-/* Execution pipeline (both bit-identical):
- *   OM_PIPELINE_WAVEFRONT  (default) per bounce one {trace -> shade -> compact} launch over SoA
- *                          path queues in HBM (bounce 0 generates the camera rays), then one
+/* Execution pipeline (all bit-identical):
+ *   OM_PIPELINE_WAVEFRONT  per bounce one {trace -> shade -> compact} launch over SoA path
+ *                          queues in HBM (bounce 0 generates the camera rays), then one
  *                          persistent tail launch, then accumulate
- *   OM_PIPELINE_MEGAKERNEL one persistent-path kernel per call */
-enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1 };
+ *   OM_PIPELINE_MEGAKERNEL one persistent-path kernel per call
+ *   OM_PIPELINE_AUTO       (default) the faster one measured for the uploaded world:
+ *                          megakernel when it has marched primitives, else wavefront */
+enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1, OM_PIPELINE_AUTO = 2 };
 om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
 /* Wavefront pipeline: bounces >= `bounce` are finished by one persistent tail launch
  * (lanes run whole remaining paths); 0 = default (16), >= max_depth = no tail.  A pure
@@ -231,6 +233,31 @@ typedef struct om_kernel_times {
 } om_kernel_times;
 om_status om_set_timing(om_ctx* ctx, int32_t enable);
 om_status om_get_kernel_times(om_ctx* ctx, om_kernel_times* out);
+
+/* ---- display views (draw_to_sdl, main.rs:345-484) ----
+ * RGB24 (row-major, W*H*3 bytes) view of the per-pixel accumulators, mode numbers as
+ * the reference's keys 0-6 (main.rs:360-367).  The blurs are apply_box_filter::<0/1/2>
+ * (main.rs:219-343); like the reference's persistent sdlpixels buffer, pixels that
+ * filter does not visit (frames with W or H == 2) keep the caller's previous bytes.
+ * Blur views need W, H >= 2. */
+enum {
+    OM_VIEW_NORMAL = 0,        /* Stats.color                                     */
+    OM_VIEW_SAMPLES = 1,       /* n / max n, gamma-quantised                      */
+    OM_VIEW_SAMPLE_BLUR = 2,   /* 3x3 blur weighted by n                          */
+    OM_VIEW_DEPTH = 3,         /* avg_depth / max finite avg_depth; sky = green  */
+    OM_VIEW_DEPTH_BLUR = 4,    /* 3x3 blur weighted by 1/(1+|depth difference|)   */
+    OM_VIEW_IDS = 5,           /* u64_to_color(scramble(bloom)) (utils.rs:46-70)  */
+    OM_VIEW_ID_BLUR = 6        /* 3x3 blur over pixels whose bloom contains ours  */
+};
+/* Device buffers on ctx's device; asynchronous on `stream` (NULL = ctx's stream). */
+om_status om_display_device(om_ctx* ctx, const om_pixel_stats* dev_stats, uint32_t width, uint32_t height, int32_t view,
+                            uint8_t* dev_rgb, void* stream);
+/* Host buffers (copies both ways, synchronous); rgb is read-modify-write. */
+om_status om_display(om_ctx* ctx, const om_pixel_stats* stats, uint32_t width, uint32_t height, int32_t view, uint8_t* rgb);
+/* Image writers for headless runs (the F12 BMP save, main.rs:473-476): 24-bit BMP
+ * (bottom-up BGR rows padded to 4 bytes, 54-byte header) and binary PPM (P6). */
+om_status om_write_bmp(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
+om_status om_write_ppm(const char* path, const uint8_t* rgb, uint32_t width, uint32_t height);
 
 #ifdef __cplusplus
 }

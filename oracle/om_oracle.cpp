@@ -657,6 +657,108 @@ static bool stats_add(PixelStats& st, V3 x, float depth, uint64_t obj_id) {
     return done;
 }
 
+
+// ----------------------------------------------------------------------------
+// main.rs:219-437 — the draw_to_sdl view modes over the pixel Stats (RGB24 out).
+// Pixels apply_box_filter does not reach (W or H == 2: main.rs:322-341 loops) keep
+// the caller's previous bytes, as the reference's persistent sdlpixels buffer does.
+// ----------------------------------------------------------------------------
+static const float SQRT2_INV_F = 0.7071067811865475244f;                                    // utils.rs:31
+static inline V3 stats_sum(const PixelStats& p) { return v3(p.sum[0], p.sum[1], p.sum[2]); }
+static inline void put_rgb(uint8_t* rgb, size_t px, V3 c) { to_u8x3(normalize_color(c), rgb + 3 * px); }
+static inline void u64_to_color(uint64_t id, uint8_t* o) {                                  // utils.rs:59-70
+    uint8_t b[8];
+    for (int k = 0; k < 8; ++k) b[k] = (uint8_t)((id >> (8 * k)) & 0xFF);
+    o[0] = b[0] ^ b[7] ^ b[3]; o[1] = b[1] ^ b[4] ^ b[5]; o[2] = b[2] ^ b[6];
+}
+// apply_box_filter_ij_samples / _depth / _id (main.rs:219-312)
+static void box_filter_ij(int mode, const PixelStats* P, uint32_t W, uint8_t* rgb, uint32_t i, uint32_t j,
+                          int min_x, int max_x, int min_y, int max_y) {
+    const size_t me = (size_t)i + (size_t)j * W;
+    const float di = P[me].avg_depth;
+    if (mode == 1 && std::isinf(di)) {                                                      // :250-257
+        std::memcpy(rgb + 3 * me, P[me].color, 3);
+        return;
+    }
+    const uint64_t state = P[me].bloom;
+    float total_weight = 0.0f;
+    V3 color = v3(0.0f, 0.0f, 0.0f);
+    for (int y = min_y; y <= max_y; ++y) {
+        for (int x = min_x; x <= max_x; ++x) {
+            const PixelStats& q = P[(size_t)((int)i + x) + (size_t)((int)j + y) * W];
+            const float is_diagonal = (x != 0 && y != 0) ? 1.0f : 0.0f;
+            if (mode == 0) {
+                const float n = (float)q.n;
+                const float diag_w = 1.0f - (1.0f - SQRT2_INV_F) * is_diagonal;
+                total_weight = total_weight + n * diag_w;
+                color = color + stats_sum(q) * diag_w;
+            } else {
+                float w;
+                if (mode == 1) {
+                    w = 1.0f / (1.0f + std::fabs(q.avg_depth - di));
+                } else {
+                    const float same_value = (q.bloom == state) ? 1.0f : 0.0f;
+                    const float partial_value = ((q.bloom & state) == state) ? 1.0f : 0.0f;
+                    w = same_value + partial_value;
+                }
+                const float diag_w = w * (1.0f - (1.0f - SQRT2_INV_F) * is_diagonal);
+                total_weight = total_weight + diag_w;
+                const V3 c = stats_sum(q) / (float)q.n;
+                color = color + diag_w * c;
+            }
+        }
+    }
+    put_rgb(rgb, me, color / total_weight);
+}
+// apply_box_filter::<MODE> (main.rs:322-343), same visiting pattern
+static void box_filter(int mode, const PixelStats* P, uint32_t H, uint32_t W, uint8_t* rgb) {
+    for (uint32_t j = 1; j + 1 < H; ++j) {
+        for (uint32_t i = 1; i + 1 < W; ++i) {
+            if (j == 1) {
+                box_filter_ij(mode, P, W, rgb, i, 0, -1, 1, 0, 1);
+                box_filter_ij(mode, P, W, rgb, i, H - 1, -1, 1, -1, 0);
+            }
+            box_filter_ij(mode, P, W, rgb, i, j, -1, 1, -1, 1);
+        }
+        box_filter_ij(mode, P, W, rgb, 0, j, 0, 1, -1, 1);
+        box_filter_ij(mode, P, W, rgb, W - 1, j, -1, 0, -1, 1);
+    }
+    box_filter_ij(mode, P, W, rgb, 0, 0, 0, 1, 0, 1);
+    box_filter_ij(mode, P, W, rgb, W - 1, 0, -1, 0, 0, 1);
+    box_filter_ij(mode, P, W, rgb, 0, H - 1, 0, 1, -1, 0);
+    box_filter_ij(mode, P, W, rgb, W - 1, H - 1, -1, 0, -1, 0);
+}
+// draw_to_sdl's mode switch (main.rs:372-437)
+static void display(const PixelStats* P, uint32_t W, uint32_t H, int mode, uint8_t* rgb) {
+    const size_t N = (size_t)W * H;
+    if (mode == 0) {                                                                        // MODE_NORMAL
+        for (size_t k = 0; k < N; ++k) std::memcpy(rgb + 3 * k, P[k].color, 3);
+    } else if (mode == 1) {                                                                 // MODE_SHOW_SAMPLES
+        uint32_t max_samples = 1;
+        for (size_t k = 0; k < N; ++k) if (P[k].n > max_samples) max_samples = P[k].n;
+        for (size_t k = 0; k < N; ++k) {
+            const float s = (float)P[k].n / (float)max_samples;
+            put_rgb(rgb, k, v3(s, s, s));
+        }
+    } else if (mode == 3) {                                                                 // MODE_SHOW_DEPTH
+        float max_depth = -1.0f;
+        for (size_t k = 0; k < N; ++k) {
+            const float d = P[k].avg_depth;
+            if (d > max_depth && !std::isinf(d)) max_depth = d;
+        }
+        for (size_t k = 0; k < N; ++k) {
+            const float d01 = P[k].avg_depth / max_depth;
+            const bool is_inf = std::isinf(d01);
+            const float rb = is_inf ? 0.0f : d01, g = is_inf ? 1.0f : d01;
+            put_rgb(rgb, k, v3(rb, g, rb));
+        }
+    } else if (mode == 5) {                                                                 // MODE_SHOW_IDS
+        for (size_t k = 0; k < N; ++k) u64_to_color(scramble(P[k].bloom), rgb + 3 * k);
+    } else {                                                                                // 2 / 4 / 6: blurs
+        box_filter(mode == 2 ? 0 : (mode == 4 ? 1 : 2), P, H, W, rgb);
+    }
+}
+
 // handle_hit render_thread.rs:105-126 ; ray_color :128-143
 struct SampleResult { V3 color; float depth; uint64_t id; uint32_t segments; };
 static inline bool handle_hit(const World& w, Ray& r, V3& cur, float tmin, float tmax, PathRng& g, float& depth, uint64_t& id) {
@@ -912,6 +1014,10 @@ void oro_rng_path_draws(uint64_t seed, uint32_t pixel, uint32_t sample, uint32_t
 void oro_jitter_table(uint64_t seed, uint32_t spp, float* out) { auto jt = jitter_table(seed, spp); std::memcpy(out, jt.data(), jt.size() * 4); }
 uint64_t oro_bloom_hash(uint64_t id) { return bloom_hash(id); }
 uint64_t oro_scramble(uint64_t id) { return scramble(id); }
+// draw_to_sdl view `mode` (0..6) of W*H stats into rgb (W*H*3, read-modify-write)
+void oro_display(const void* stats, uint32_t W, uint32_t H, int32_t mode, uint8_t* rgb) {
+    display((const PixelStats*)stats, W, H, mode, rgb);
+}
 
 // --- primitive KAT surface: out = t, point3, normal3, obj_id(as float) ; returns hit ---
 static void hr_out(const HitRecord& h, float* out) { out[0] = h.t; st3(h.point, out + 1); st3(h.normal, out + 4); }

@@ -66,6 +66,7 @@ def _load():
         "oro_rng_path_draws": (None, [C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, fp]),
         "oro_jitter_table": (None, [C.c_uint64, C.c_uint32, fp]),
         "oro_bloom_hash": (C.c_uint64, [C.c_uint64]), "oro_scramble": (C.c_uint64, [C.c_uint64]),
+        "oro_display": (None, [vp, C.c_uint32, C.c_uint32, C.c_int32, vp]),
         "oro_hit_world": (C.c_int, [vp, fp, C.c_float, C.c_float, fp, C.POINTER(C.c_uint64)]),
         "oro_scatter": (None, [fp, fp, mp, C.c_uint64, fp, C.POINTER(C.c_uint64)]),
         "oro_get_ray": (None, [C.POINTER(OroCamera), C.c_float, C.c_float, C.c_uint64, fp]),
@@ -248,3 +249,13 @@ def bloom_hash(i):
 
 def scramble(i):
     return lib.oro_scramble(C.c_uint64(i))
+
+
+def display(stats, W, H, mode, rgb=None):
+    """draw_to_sdl view `mode` (main.rs:360-437) of a W*H PIXEL_STATS_DTYPE array -> (H, W, 3) uint8.
+    `rgb` (H*W*3 uint8) is updated in place, like the reference's persistent sdlpixels buffer."""
+    st = np.ascontiguousarray(stats)
+    assert st.dtype == PIXEL_STATS_DTYPE and st.size == W * H
+    out = np.zeros(W * H * 3, dtype=np.uint8) if rgb is None else rgb.reshape(-1)
+    lib.oro_display(st.ctypes.data, W, H, mode, out.ctypes.data)
+    return out.reshape(H, W, 3)

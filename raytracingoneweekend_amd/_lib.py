@@ -19,8 +19,8 @@ OM_KERNEL_AUTO, OM_KERNEL_BRUTE, OM_KERNEL_CULLED, OM_KERNEL_BVH, OM_KERNEL_SBVH
     0, 1, 2, 3, 4, 5, 6
 KERNELS = {"auto": OM_KERNEL_AUTO, "brute": OM_KERNEL_BRUTE, "culled": OM_KERNEL_CULLED, "bvh": OM_KERNEL_BVH,
            "sbvh": OM_KERNEL_SBVH, "bvh2": OM_KERNEL_BVH2, "bvh4": OM_KERNEL_BVH4}
-OM_PIPELINE_MEGAKERNEL, OM_PIPELINE_WAVEFRONT = 0, 1
-PIPELINES = {"megakernel": OM_PIPELINE_MEGAKERNEL, "wavefront": OM_PIPELINE_WAVEFRONT}
+OM_PIPELINE_MEGAKERNEL, OM_PIPELINE_WAVEFRONT, OM_PIPELINE_AUTO = 0, 1, 2
+PIPELINES = {"megakernel": OM_PIPELINE_MEGAKERNEL, "wavefront": OM_PIPELINE_WAVEFRONT, "auto": OM_PIPELINE_AUTO}
 
 F3 = C.c_float * 3
 F16 = C.c_float * 16
@@ -47,6 +47,8 @@ class om_counters(C.Structure):
 
 
 KT_CLASSES = ("bounce0", "bounce", "tail", "accumulate", "megakernel")   # OM_KT_* order
+# draw_to_sdl modes (main.rs:360-367), OM_VIEW_* order
+VIEWS = ("normal", "samples", "sample_blur", "depth", "depth_blur", "ids", "id_blur")
 
 
 class om_kernel_times(C.Structure):
@@ -70,7 +72,8 @@ EXPORTS = [
     "om_world_random_scene", "om_world_basic_scene", "om_world_marched_scene", "om_create", "om_destroy",
     "om_last_error", "om_upload_world", "om_set_kernel", "om_render", "om_render_device",
     "om_render_device_pixels", "om_get_counters", "om_reset_counters", "om_set_counting", "om_set_pipeline",
-    "om_set_tail_bounce", "om_set_timing", "om_get_kernel_times",
+    "om_set_tail_bounce", "om_set_timing", "om_get_kernel_times", "om_display_device", "om_display",
+    "om_write_bmp", "om_write_ppm",
 ]
 
 
@@ -148,6 +151,10 @@ def _load():
         "om_set_tail_bounce": (st, [vp, C.c_uint32]),
         "om_set_timing": (st, [vp, C.c_int32]),
         "om_get_kernel_times": (st, [vp, C.POINTER(om_kernel_times)]),
+        "om_display_device": (st, [vp, vp, C.c_uint32, C.c_uint32, C.c_int32, vp, vp]),
+        "om_display": (st, [vp, vp, C.c_uint32, C.c_uint32, C.c_int32, vp]),
+        "om_write_bmp": (st, [C.c_char_p, vp, C.c_uint32, C.c_uint32]),
+        "om_write_ppm": (st, [C.c_char_p, vp, C.c_uint32, C.c_uint32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

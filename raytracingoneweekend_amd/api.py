@@ -285,7 +285,7 @@ class HittableList:
         check(lib.om_world_export(self._w, int(kind), int(index), fptr(out), n))
         return np.array(list(out), dtype=np.float32)
 
-    def freeze(self, cam=None, device=0, kernel="auto", pipeline="wavefront"):
+    def freeze(self, cam=None, device=0, kernel="auto", pipeline="auto"):
         """hits.rs:87-89: snapshot to device memory (the camera is unused: the camera hash is out of scope)."""
         return FrozenHittableList(self, device=device, kernel=kernel, pipeline=pipeline)
 
@@ -293,7 +293,7 @@ class HittableList:
 class FrozenHittableList:
     """hits.rs:63-69 — a world resident in HBM on one device (om_ctx)."""
 
-    def __init__(self, world, device=0, kernel="auto", pipeline="wavefront"):
+    def __init__(self, world, device=0, kernel="auto", pipeline="auto"):
         self._ctx = C.c_void_p()
         check(lib.om_create(int(device), C.byref(self._ctx)))
         check(lib.om_upload_world(self._ctx, world.handle), self._ctx)
@@ -381,3 +381,32 @@ def render(camera, world, max_depth, tmin, tmax, samples_per_pixel, image_width,
     if samples_atom is not None:
         samples_atom[0] += out["credited"]
     return out
+
+
+# ---------------------------------------------------------------- main.rs draw_to_sdl
+def display(frozen, pixels_box, image_width, image_height, view="normal", rgb=None):
+    """One draw_to_sdl view (main.rs:360-437) of the framebuffer, computed on the device
+    of `frozen` -> (H, W, 3) uint8 RGB.  `view`: a name of _lib.VIEWS or 0-6 (the
+    reference's keypad modes).  Pass the previous `rgb` to keep the reference's
+    behaviour for pixels its box filter never visits (W or H == 2)."""
+    st = pixels_box.pixels if isinstance(pixels_box, PixelsBox) else pixels_box
+    st = np.ascontiguousarray(st)
+    W, H = int(image_width), int(image_height)
+    if st.dtype != L.PIXEL_STATS_DTYPE or st.size != W * H:
+        raise ValueError("display: need W*H om_pixel_stats")
+    mode = L.VIEWS.index(view) if isinstance(view, str) else int(view)
+    out = np.zeros(W * H * 3, dtype=np.uint8) if rgb is None else np.ascontiguousarray(rgb, dtype=np.uint8).reshape(-1).copy()
+    check(lib.om_display(frozen.ctx, st.ctypes.data, W, H, mode, out.ctypes.data), frozen.ctx)
+    return out.reshape(H, W, 3)
+
+
+def write_bmp(path, rgb):
+    """24-bit BMP of an (H, W, 3) uint8 image (the F12 save, main.rs:473-476)."""
+    a = np.ascontiguousarray(rgb, dtype=np.uint8)
+    check(lib.om_write_bmp(str(path).encode(), a.ctypes.data, a.shape[1], a.shape[0]))
+
+
+def write_ppm(path, rgb):
+    """Binary PPM (P6) of an (H, W, 3) uint8 image."""
+    a = np.ascontiguousarray(rgb, dtype=np.uint8)
+    check(lib.om_write_ppm(str(path).encode(), a.ctypes.data, a.shape[1], a.shape[0]))

@@ -23,6 +23,7 @@
 #include "../../include/ottomarcher.h"
 #include "om_device.h"
 #include "om_layout.h"
+#include "om_display.h"
 #include "om_wavefront.h"
 #include "om_world.h"
 
@@ -238,11 +239,11 @@ struct om_ctx {
     OmSceneDev scene{};
     bool have_world = false;
     int kernel = OM_KERNEL_AUTO;
-    DevBuf counters, jitter, stats, pixels;
+    DevBuf counters, jitter, stats, pixels, view_scratch, view_rgb;
     uint64_t jitter_seed = 0; uint32_t jitter_spp = 0;
     hipStream_t last_stream = nullptr;
     bool count_work = true;
-    int pipeline = OM_PIPELINE_WAVEFRONT;
+    int pipeline = OM_PIPELINE_AUTO;
     uint32_t tail_bounce = 0;
     omw::Timer timer;
     omw::Buffers wf;
@@ -251,6 +252,7 @@ struct om_ctx {
     ~om_ctx() {
         for (auto& b : scene_bufs) b.release();
         counters.release(); jitter.release(); stats.release(); pixels.release(); frame_list.release();
+        view_scratch.release(); view_rgb.release();
         wf.release();
         timer.release();
         if (stream) (void)hipStreamDestroy(stream);
@@ -374,9 +376,12 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         threads = tiles * 64u;
     }
     if (threads == 0) return OM_OK;
+    int pipeline = c->pipeline;
+    if (pipeline == OM_PIPELINE_AUTO)   // C2 (marched SDFs): megakernel 741 vs wavefront 555 Msamples/s
+        pipeline = (c->scene.n_msph + c->scene.n_mbox + c->scene.n_mtor) ? OM_PIPELINE_MEGAKERNEL : OM_PIPELINE_WAVEFRONT;
     int mode = c->kernel;
-    if (mode == OM_KERNEL_AUTO) mode = c->pipeline == OM_PIPELINE_WAVEFRONT ? OM_KERNEL_BVH2 : OM_KERNEL_BVH;
-    if (c->pipeline == OM_PIPELINE_WAVEFRONT) {
+    if (mode == OM_KERNEL_AUTO) mode = pipeline == OM_PIPELINE_WAVEFRONT ? OM_KERNEL_BVH2 : OM_KERNEL_BVH;
+    if (pipeline == OM_PIPELINE_WAVEFRONT) {
         omw::Launch L;
         L.S = c->scene; L.C = C; L.P = P;
         L.jitter = (const float2*)c->jitter.p;
@@ -582,7 +587,7 @@ om_status om_get_counters(om_ctx* c, om_counters* out) {
 
 om_status om_set_pipeline(om_ctx* c, int32_t pipeline) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
-    if (pipeline != OM_PIPELINE_MEGAKERNEL && pipeline != OM_PIPELINE_WAVEFRONT)
+    if (pipeline != OM_PIPELINE_MEGAKERNEL && pipeline != OM_PIPELINE_WAVEFRONT && pipeline != OM_PIPELINE_AUTO)
         return set_err(c, OM_ERR_INVALID, "om_set_pipeline: unknown pipeline");
     c->pipeline = pipeline;
     return OM_OK;
@@ -618,6 +623,43 @@ om_status om_get_kernel_times(om_ctx* c, om_kernel_times* out) {
         out->ms[t.cls[i]] += (double)ms;
     }
     t.cls.clear();
+    return OM_OK;
+}
+
+om_status om_display_device(om_ctx* c, const om_pixel_stats* dev_stats, uint32_t width, uint32_t height, int32_t view,
+                            uint8_t* dev_rgb, void* stream) {
+    if (!c || !dev_stats || !dev_rgb) return set_err(c, OM_ERR_INVALID, "om_display_device: null argument");
+    if (view < OM_VIEW_NORMAL || view > OM_VIEW_ID_BLUR) return set_err(c, OM_ERR_INVALID, "om_display_device: unknown view");
+    if (width == 0 || height == 0 || (uint64_t)width * height > 0xFFFFFFFFull / 3u)
+        return set_err(c, OM_ERR_INVALID, "om_display_device: bad frame size");
+    const bool blur = view == OM_VIEW_SAMPLE_BLUR || view == OM_VIEW_DEPTH_BLUR || view == OM_VIEW_ID_BLUR;
+    if (blur && (width < 2 || height < 2))   // apply_box_filter indexes a 2x2 corner neighbourhood
+        return set_err(c, OM_ERR_INVALID, "om_display_device: blur views need width, height >= 2");
+    OM_HIP(c, hipSetDevice(c->device));
+    om_status s = ensure(c, c->view_scratch, omv::scratch_bytes(width, height));
+    if (s != OM_OK) return s;
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    const hipError_t e = omv::render(dev_stats, width, height, view, dev_rgb, c->view_scratch.p, st);
+    if (e != hipSuccess) return set_err(c, OM_ERR_DEVICE, std::string("om_display_device: ") + hipGetErrorString(e));
+    c->last_stream = st;
+    return OM_OK;
+}
+
+om_status om_display(om_ctx* c, const om_pixel_stats* stats, uint32_t width, uint32_t height, int32_t view, uint8_t* rgb) {
+    if (!c || !stats || !rgb) return set_err(c, OM_ERR_INVALID, "om_display: null argument");
+    if (width == 0 || height == 0 || (uint64_t)width * height > 0xFFFFFFFFull / 3u)
+        return set_err(c, OM_ERR_INVALID, "om_display: bad frame size");
+    OM_HIP(c, hipSetDevice(c->device));
+    const size_t npx = (size_t)width * height;
+    om_status s = ensure(c, c->stats, npx * sizeof(om_pixel_stats));
+    if (s != OM_OK) return s;
+    if ((s = ensure(c, c->view_rgb, npx * 3)) != OM_OK) return s;
+    OM_HIP(c, hipMemcpyAsync(c->stats.p, stats, npx * sizeof(om_pixel_stats), hipMemcpyHostToDevice, c->stream));
+    OM_HIP(c, hipMemcpyAsync(c->view_rgb.p, rgb, npx * 3, hipMemcpyHostToDevice, c->stream));
+    if ((s = om_display_device(c, (const om_pixel_stats*)c->stats.p, width, height, view, (uint8_t*)c->view_rgb.p, c->stream)) != OM_OK)
+        return s;
+    OM_HIP(c, hipMemcpyAsync(rgb, c->view_rgb.p, npx * 3, hipMemcpyDeviceToHost, c->stream));
+    OM_HIP(c, hipStreamSynchronize(c->stream));
     return OM_OK;
 }
 

@@ -22,7 +22,7 @@ STRUCTS = {
     "om_pixel_stats": ["bloom", "sum", "n", "avg_depth", "bad_avgs", "color", "flags", "reserved"],
 }
 ENUMS = ["OM_LAMBERTIAN", "OM_METAL", "OM_DIELECTRIC", "OM_KERNEL_AUTO", "OM_KERNEL_BRUTE", "OM_KERNEL_CULLED",
-         "OM_KERNEL_BVH", "OM_KERNEL_SBVH", "OM_KERNEL_BVH2", "OM_KERNEL_BVH4", "OM_PIPELINE_MEGAKERNEL", "OM_PIPELINE_WAVEFRONT",
+         "OM_KERNEL_BVH", "OM_KERNEL_SBVH", "OM_KERNEL_BVH2", "OM_KERNEL_BVH4", "OM_PIPELINE_MEGAKERNEL", "OM_PIPELINE_WAVEFRONT", "OM_PIPELINE_AUTO",
          "OM_KT_BOUNCE0", "OM_KT_BOUNCE", "OM_KT_TAIL", "OM_KT_ACCUMULATE", "OM_KT_MEGAKERNEL", "OM_KT_N",
          "OM_OK", "OM_ERR_INVALID", "OM_ERR_DEVICE", "OM_ERR_STATE", "OM_ERR_UNSUPPORTED", "OM_ERR_NOMEM",
          "OM_ABI_VERSION"]
@@ -85,4 +85,5 @@ def test_enum_values_match_binding(om, c_layout):
         assert _lib.KERNELS[name] == c_layout[const], name
     assert _lib.PIPELINES["megakernel"] == c_layout["OM_PIPELINE_MEGAKERNEL"]
     assert _lib.PIPELINES["wavefront"] == c_layout["OM_PIPELINE_WAVEFRONT"]
+    assert _lib.PIPELINES["auto"] == c_layout["OM_PIPELINE_AUTO"]
     assert np.array_equal([c_layout[k] for k in ("OM_LAMBERTIAN", "OM_METAL", "OM_DIELECTRIC")], [0, 1, 2])
