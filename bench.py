@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--pipeline", default="auto", choices=list(L.PIPELINES))
     ap.add_argument("--tail", type=int, default=0, help="first bounce of the persistent tail launch (0 = library default)")
     ap.add_argument("--no-kernel-timing", action="store_true", help="no per-launch HIP events in the timed region")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, the measured path); gloo gathers through host memory and maps "
+                         "ranks onto the visible GPUs (a functional rehearsal of N>1 on a 1-GPU box)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -116,9 +119,15 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
+    gloo = args.dist_backend == "gloo"
+    if gloo:
+        local_rank = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local_rank)
     if world_size > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if gloo:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     # ---- setup (not timed): scene build + freeze/upload, camera, tile lists
     # a dedicated (non-NULL) stream: the kernel, its HIP events and the collectives all run on it
@@ -156,7 +165,7 @@ def main():
     gathered, send = None, None
     if world_size > 1:                                       # gather buffers (equal-size shards), allocated untimed
         n_max = shard.shard_capacity(W, H, world_size) * 40
-        send = torch.zeros(n_max, dtype=torch.uint8, device="cuda")
+        send = torch.zeros(n_max, dtype=torch.uint8, device="cpu" if gloo else "cuda")
         gathered = [torch.empty_like(send) for _ in range(world_size)] if rank == 0 else None
     torch.cuda.synchronize()
 
@@ -172,7 +181,7 @@ def main():
     for k in range(args.steps):
         step(p)
     if world_size > 1:                                       # RCCL gather of the f32 framebuffer to rank 0
-        send[: stats.numel()] = stats
+        send[: stats.numel()] = stats.cpu() if gloo else stats
         dist.gather(send, gathered, dst=0)
     torch.cuda.synchronize()
     if world_size > 1:
@@ -180,7 +189,7 @@ def main():
     elapsed = time.perf_counter() - t0
     # ---- end timed region
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else "cuda")
     if world_size > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -255,7 +264,8 @@ def main():
             "config": {"workload": f"{args.config} {cfg['scene']} {W}x{H}, {spp_total} spp timed ({spp_step} spp/step), "
                                    f"depth {MAX_DEPTH}" + (f", {cfg['march_steps']} march steps" if args.config == "C2" else ""),
                        "width": W, "height": H, "spp_per_step": spp_step, "max_depth": MAX_DEPTH,
-                       "parallelism": f"tile{world_size}", "kernel": args.kernel,
+                       "parallelism": f"tile{world_size}" + ("/gloo" if gloo and world_size > 1 else ""),
+                       "kernel": args.kernel,
                        "pipeline": args.pipeline + (("->megakernel" if mega else "->wavefront") if args.pipeline == "auto" else ""),
                        "tail_bounce": args.tail or "default"},
             "hbm_gbs": hbm_gbs,
