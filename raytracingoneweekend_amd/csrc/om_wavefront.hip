@@ -72,7 +72,10 @@ template <int TR>
 __host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
     return kBlk * ((TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) ? S.b4_stack : S.b2_stack) * 2u;
 }
-constexpr uint32_t kTailSpb = 4;                                  // queue segments per tail workgroup
+#ifndef OM_WF_TAIL_SPB
+#define OM_WF_TAIL_SPB 4
+#endif
+constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
 
 extern __shared__ __attribute__((aligned(16))) uint4 wf_lds[];

@@ -21,6 +21,8 @@ declare -A V=(
   [b1024w8]="$COMMON $DEV -DOM_WF_BLOCK=1024 -DOM_WF_WAVES=8"
   # cost split of the fused bounce kernel: run one half twice
   [trace2x]="$COMMON $DEV -DOM_ABLATE_TRACE2X"
+  [tspb1]="$COMMON $DEV -DOM_WF_TAIL_SPB=1"
+  [tspb2]="$COMMON $DEV -DOM_WF_TAIL_SPB=2"
   [shade2x]="$COMMON $DEV -DOM_ABLATE_SHADE2X"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
@@ -47,7 +49,7 @@ mkdir -p "$OUT"
 : > "$OUT/abl.jsonl"
 for k in ${VARIANTS:-base fastdiv contract rng32 ftz}; do
   echo "{\"variant\": \"$k\"}" >> "$OUT/abl.jsonl"
-  OM_LIB=$PWD/_abl/lib_$k.so timeout -k 10 200 python bench.py --steps 8 --warmup 1 --no-cpu-baseline "${@:3}" \
+  OM_LIB=$PWD/_abl/lib_$k.so timeout -k 10 200 python bench.py --steps ${STEPS:-8} --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} "${@:3}" \
       >> "$OUT/abl.jsonl" 2>> "$OUT/abl.err" || { echo "variant $k failed"; exit 1; }
 done
 echo ok
