@@ -215,6 +215,14 @@ om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
  * scheduling knob: results are bit-identical for every value. */
 om_status om_set_tail_bounce(om_ctx* ctx, uint32_t bounce);
 
+/* Primary rays (wavefront, BVH2): bounce 0 can test, per 8x8 pixel tile, only the leaf
+ * records a conservative lens-aware frustum of the tile reaches, instead of traversing
+ * the BVH (the conservative form of the reference's camera hash, camera_hash.rs;
+ * DESIGN.md §5.10).  Results are bit-identical either way.
+ *   OM_PRIMARY_LISTS_AUTO (default) when a pixel sees <= 12 candidates on average */
+enum { OM_PRIMARY_LISTS_OFF = 0, OM_PRIMARY_LISTS_AUTO = 1, OM_PRIMARY_LISTS_ON = 2 };
+om_status om_set_primary_lists(om_ctx* ctx, int32_t mode);
+
 /* Per-kernel-class device time: while enabled, every launch is bracketed by a HIP event
  * pair on its stream (bench.py's roofline uses it).  om_get_kernel_times synchronises
  * the last recorded event, returns the totals since the previous read (or since

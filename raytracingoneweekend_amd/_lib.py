@@ -73,7 +73,7 @@ EXPORTS = [
     "om_last_error", "om_upload_world", "om_set_kernel", "om_render", "om_render_device",
     "om_render_device_pixels", "om_get_counters", "om_reset_counters", "om_set_counting", "om_set_pipeline",
     "om_set_tail_bounce", "om_set_timing", "om_get_kernel_times", "om_display_device", "om_display",
-    "om_write_bmp", "om_write_ppm",
+    "om_write_bmp", "om_write_ppm", "om_set_primary_lists",
 ]
 
 
@@ -155,6 +155,7 @@ def _load():
         "om_display": (st, [vp, vp, C.c_uint32, C.c_uint32, C.c_int32, vp]),
         "om_write_bmp": (st, [C.c_char_p, vp, C.c_uint32, C.c_uint32]),
         "om_write_ppm": (st, [C.c_char_p, vp, C.c_uint32, C.c_uint32]),
+        "om_set_primary_lists": (st, [vp, C.c_int32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -304,6 +304,17 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
         for (uint32_t c : {fw.b2nodes[i].c0, fw.b2nodes[i].c1})
             if (!(c & OM_LEAF)) { depth[c] = depth[i] + 1; fw.b2_depth = std::max(fw.b2_depth, depth[c]); }
     }
+    // conservative world box of every leaf record (the tree's own item boxes)
+    fw.srec_box.clear();
+    for (const OmAffineTest& t : fw.srecs) {
+        uint32_t tag;
+        std::memcpy(&tag, &t.pad, 4);
+        const uint32_t gi = tag & 0x7FFFFFFFu;
+        const Box bx = (tag >> 31) ? affine_box(w.cubes[gi - fw.offsets[K_CUBE]].l2w, 0.5)
+                                   : affine_box(w.spheres[gi].l2w, -1.0);
+        for (int i = 0; i < 3; ++i) fw.srec_box.push_back(std::nextafter((float)bx.lo[i], -INFINITY));
+        for (int i = 0; i < 3; ++i) fw.srec_box.push_back(std::nextafter((float)bx.hi[i], INFINITY));
+    }
     build_bvh4(fw);
 }
 

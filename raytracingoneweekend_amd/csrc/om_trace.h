@@ -146,23 +146,27 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
     }
 }
 
-// Leaf of the BVH2/BVH4: its Sphere/Cube records, tested in place (tag bit 31 = cube).
+// One leaf record (Sphere/Cube test record, tag bit 31 = cube), brute-force tie rule.
+template <class Wk>
+__device__ __forceinline__ void test_rec(const OmAffineTest& R, F3 o, F3 d, float tmin, float& closest, int& best, Wk& w) {
+    uint32_t tag;
+    __builtin_memcpy(&tag, &R.pad, 4);
+    const uint32_t gi = tag & 0x7FFFFFFFu;
+    float t;
+    int ax;
+    w.add_prim();
+    const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root(R, o, d, tmin, closest, t);
+    if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
+}
+
+// Leaf of the BVH2/BVH4: its records, tested in place.
 template <class Wk>
 __device__ __forceinline__ void test_leaf(const OmAffineTest* recs, uint32_t lf, F3 o, F3 d, float tmin, float& closest,
                                           int& best, Wk& w) {
     const uint32_t first = lf >> 8, cnt = lf & 255u;
-    for (uint32_t k = 0; k < cnt; ++k) {
-        const OmAffineTest R = recs[first + k];
-        uint32_t tag;
-        __builtin_memcpy(&tag, &R.pad, 4);
-        const uint32_t gi = tag & 0x7FFFFFFFu;
-        float t;
-        int ax;
-        w.add_prim();
-        const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root(R, o, d, tmin, closest, t);
-        if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
-    }
+    for (uint32_t k = 0; k < cnt; ++k) test_rec(recs[first + k], o, d, tmin, closest, best, w);
 }
+
 
 // Stackless BVH traversal.  Nodes are visited in depth-first
 // order: box hit -> next node (internal) or the leaf's records then `skip`; miss ->
@@ -343,6 +347,24 @@ __device__ __forceinline__ int nonfinite_hit(const OmSceneDev& S, float& closest
     if (S.n_plane) { closest = __int_as_float(0x7FC00000); return (int)(S.off_plane + S.n_plane - 1u); }
     if (S.n_sph) { closest = __int_as_float(0x7FC00000); return (int)(S.n_sph - 1u); }
     return -1;
+}
+
+// Primary ray with a per-tile candidate list (om_tiles.h): always2, then
+// every record the conservative lens-aware frustum of its 8x8 tile can reach — the
+// brute-force loop of hits.rs:274-285 over a superset of the records it could accept.
+template <class Wk>
+__device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t* toff, const uint16_t* tidx, uint32_t tile,
+                                            F3 o, F3 d, float tmin, float& closest, Wk& w) {
+    if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
+    int best = -1;
+    const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
+    const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
+    const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
+    offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, tmin * 0.5f - 1e-3f, closest, best, w);
+    const uint32_t e = toff[tile + 1];
+    for (uint32_t k = toff[tile]; k < e; ++k) test_rec(S.srecs[tidx[k]], o, d, tmin, closest, best, w);
+    return best;
 }
 
 template <int DEPTH, int STRIDE, class Wk>

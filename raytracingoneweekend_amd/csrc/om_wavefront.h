@@ -61,6 +61,8 @@ struct Launch {
     int trace_mode;              // closest-hit kernel variant (om_render.hip MODE_*)
     uint32_t tail_bounce;        // first bounce run by the persistent tail kernel (0 = default)
     Timer* timer;                // per-launch event timing (may be off)
+    const uint32_t* tile_off;    // primary-ray candidate lists per 8x8 tile (null = traverse the BVH)
+    const uint16_t* tile_idx;
 };
 
 // Renders P.sample_count samples of every listed pixel; returns 0 or a HIP error text.

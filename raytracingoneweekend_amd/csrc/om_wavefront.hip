@@ -128,6 +128,8 @@ struct Gen {
     const om_pixel_stats* stats;
     const uint32_t* pixels;      // tile-ordered pixel list
     uint32_t n_pixels, by_pixel, batch;
+    const uint32_t* tile_off;    // primary-ray candidate lists (null: traverse)
+    const uint16_t* tile_idx;
 };
 
 // A path between bounces: ray_color's loop state (render_thread.rs:128-143).
@@ -274,12 +276,14 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
         const uint32_t jj = base + threadIdx.x;
         bool keep = false;
         Path p;
+        uint32_t p_pixel = 0;
         if (jj < n) {
             const uint64_t i = seg0 + jj;
             bool live = true;
             if (FIRST) {
                 const uint32_t s_local = (uint32_t)(i / R.n_pixels), k = (uint32_t)(i - (uint64_t)s_local * R.n_pixels);
                 const uint32_t pixel = R.pixels[k];
+                p_pixel = pixel;
                 const om_pixel_stats& ps = R.stats[R.by_pixel ? pixel : k];
                 const uint32_t s = ps.n + s_local;
                 live = s < P.spp_total && !(P.adaptive && (ps.flags & 1u));
@@ -296,7 +300,20 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
             }
             if (live) {
                 float closest;
-                const int best = trace<TR, MARCH>(S, P, T, p.o, p.d, closest, w);
+                int best;
+                if (FIRST && (TR == TR_BVH2_LDS || TR == TR_BVH2_GLOBAL) && R.tile_off) {
+                    const uint32_t line = p_pixel / P.width;
+                    const uint32_t tile = (p_pixel - line * P.width) / 8u + (line / 8u) * P.tiles_x;
+                    closest = P.tmax;
+                    best = traced_tiles(S, R.tile_off, R.tile_idx, tile, p.o, p.d, P.tmin, closest, w);
+                    if (MARCH) {
+                        float tm;
+                        const int mg = march(S, p.o, p.d, P.tmin, P.tmax, closest, P.march_steps, tm, w);
+                        if (mg >= 0) { best = mg; closest = tm; }
+                    }
+                } else {
+                    best = trace<TR, MARCH>(S, P, T, p.o, p.d, closest, w);
+                }
 #ifdef OM_ABLATE_TRACE2X   // timing ablation (tools/ablate.sh): the trace runs twice, same answer
                 {
                     F3 o2 = p.o;
@@ -515,6 +532,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     Gen R;
     R.C = L.C; R.jitter = L.jitter; R.stats = L.stats; R.pixels = L.pixels; R.n_pixels = n_px;
     R.by_pixel = L.stats_by_pixel ? 1u : 0u;
+    R.tile_off = L.tile_off; R.tile_idx = L.tile_idx;
     for (uint32_t done = 0; done < L.P.sample_count;) {
         const uint32_t b = std::min(batch, L.P.sample_count - done);
         const uint64_t paths = (uint64_t)n_px * b;

@@ -40,6 +40,7 @@ struct FrozenWorld {
     std::vector<OmAffineTest> srecs;   // its records in leaf order
     std::vector<uint32_t> always2;     // prims outside the stackless BVH
     std::vector<OmAlwaysRec> always2_rec;  // the same, with their conservative boxes
+    std::vector<float> srec_box;       // per srec: inflated box lo xyz, hi xyz (primary-ray tile lists)
     std::vector<OmBvh2Node> b2nodes;   // compressed BVH2 (same leaves/records as snodes)
     std::vector<uint32_t> b2leaves;    // its leaf table: (first_record << 8) | count
     uint32_t b2_depth = 0;             // its depth (stack bound)

@@ -211,3 +211,36 @@ def test_auto_pipeline_choice(om, oracle):
         exp, _ = oracle.render(oworld, oracle.default_camera(W / H), oracle.params(W, H, 2, seed=8, march_steps=256))
         nb, msg = compare_stats(pix.pixels, exp, f"auto/{want}")
         assert nb == 0, msg
+
+
+def _render_lists(om, world, cam, W, H, spp, lists, seed=12, march_steps=1024):
+    from raytracingoneweekend_amd import _lib as L
+    fz = world.freeze(cam, pipeline="wavefront")
+    L.check(L.lib.om_set_primary_lists(fz.ctx, lists), fz.ctx)
+    pix = om.PixelsBox.new(W * H)
+    om.render(cam, fz, 50, 0.001, 100.0, spp, W, H, pix, seed=seed, march_steps=march_steps)
+    return pix.pixels
+
+
+@pytest.mark.parametrize("scene", ["traced", "full", "kitchen", "10k", "inside_wide_lens"])
+def test_primary_tile_lists_bit_exact(om, oracle, scene):
+    """Bounce 0 with per-tile candidate lists (forced on / off / auto) == oracle, incl. a
+    wide-aperture camera inside the sphere field (boxes behind the camera, large lens
+    parallax) and odd frame sizes (partial tiles)."""
+    W, H, SPP = 53, 37, 3
+    if scene == "kitchen":
+        w, ow, cam, ocam = kitchen_sink(om, oracle)
+    else:
+        kw = {"traced": {}, "full": {"with_torus": True}, "10k": {"grid_half": 50, "extras": False},
+              "inside_wide_lens": {}}[scene]
+        w, ow = om.random_scene(0x5EED, **kw), oracle.random_scene(0x5EED, **kw)
+        if scene == "inside_wide_lens":
+            args = ((0.3, 0.35, 0.2), (5.0, 0.2, 2.0), (0.0, 1.0, 0.0), 70.0, W / H, 1.5, 2.0)
+            cam, ocam = om.Camera.new(*args), oracle.camera(*args)
+        else:
+            cam, ocam = om.default_camera(W / H), oracle.default_camera(W / H)
+    exp, _ = oracle.render(ow, ocam, oracle.params(W, H, SPP, seed=12))
+    for lists in (2, 0, 1):
+        got = _render_lists(om, w, cam, W, H, SPP, lists)
+        nb, msg = compare_stats(got, exp, f"lists{lists}/{scene}")
+        assert nb == 0, msg

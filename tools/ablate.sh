@@ -37,7 +37,7 @@ fi
 if [ "$1" = build ]; then
   mkdir -p _abl
   for k in "${!V[@]}"; do
-    ( /opt/rocm/bin/hipcc ${V[$k]} -shared -o _abl/lib_$k.so $SRC/om_world.cpp $SRC/om_bvh.cpp $SRC/om_image.cpp -x hip $SRC/om_render.hip $SRC/om_wavefront.hip $SRC/om_display.hip \
+    ( /opt/rocm/bin/hipcc ${V[$k]} -shared -o _abl/lib_$k.so $SRC/om_world.cpp $SRC/om_bvh.cpp $SRC/om_image.cpp $SRC/om_tiles.cpp -x hip $SRC/om_render.hip $SRC/om_wavefront.hip $SRC/om_display.hip \
       > _abl/$k.log 2>&1 && echo "built $k" ) &
   done
   wait
