@@ -103,7 +103,9 @@ def main():
     ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
     ap.add_argument("--pipeline", default="auto", choices=list(L.PIPELINES))
     ap.add_argument("--tail", type=int, default=0, help="first bounce of the persistent tail launch (0 = library default)")
-    ap.add_argument("--no-kernel-timing", action="store_true", help="no per-launch HIP events in the timed region")
+    ap.add_argument("--kernel-timing", default="span", choices=["span", "launch", "off"],
+                    help="HIP events in the timed region: span = once around each batch's bounce kernels "
+                         "(2 events/step, default), launch = around every launch (per-kernel breakdown)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the measured path); gloo gathers through host memory and maps "
                          "ranks onto the visible GPUs (a functional rehearsal of N>1 on a 1-GPU box)")
@@ -170,8 +172,8 @@ def main():
     torch.cuda.synchronize()
 
     kt = L.om_kernel_times()
-    timing = not args.no_kernel_timing
-    L.check(L.lib.om_set_timing(ctx, int(timing)), ctx)      # HIP events around every launch, on `stream`
+    timing = args.kernel_timing != "off"
+    L.check(L.lib.om_set_timing(ctx, {"off": 0, "launch": 1, "span": 2}[args.kernel_timing]), ctx)   # events on `stream`
 
     # ---- timed region
     if world_size > 1:
@@ -216,7 +218,12 @@ def main():
     # roofline of the dominant kernel: the fused trace+shade bounce kernel (all its launches:
     # bounce 0, bounces 1.., tail), algorithmic flops from the live counters / its event time
     mega = kt.launches[L.KT_CLASSES.index("megakernel")] > 0     # the pipeline that actually ran (auto)
-    fam = [L.KT_CLASSES.index("megakernel")] if mega else [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
+    if mega:
+        fam = [L.KT_CLASSES.index("megakernel")]
+    elif args.kernel_timing == "span":
+        fam = [L.KT_CLASSES.index("bounce_span")]
+    else:
+        fam = [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
     launches = sum(kt.launches[i] for i in fam)
     kern_s = sum(kt.ms[i] for i in fam) / 1e3
     roof = None
@@ -236,7 +243,7 @@ def main():
                 "launches_per_step": round(launches / args.steps, 2), "avg_launch_ms": round(avg_launch_s * 1e3, 4),
                 "flop_per_launch": round(flops / launches), "algorithmic_bytes_per_launch": round(nbytes / launches),
                 "hbm_achieved_gbs": round(nbytes / kern_s / 1e9, 2), "traffic_source": traffic_src,
-                "kernel_share_of_step": round(kern_s / elapsed, 4),
+                "kernel_share_of_step": round(kern_s / elapsed, 4), "timing": args.kernel_timing,
                 "all_kernels_ms_per_step": {k: round(kt.ms[i] / args.steps, 4) for i, k in enumerate(L.KT_CLASSES)
                                             if kt.launches[i]}}
     hbm_gbs = roof["hbm_achieved_gbs"] if roof else None

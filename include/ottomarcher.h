@@ -223,8 +223,10 @@ om_status om_set_tail_bounce(om_ctx* ctx, uint32_t bounce);
 enum { OM_PRIMARY_LISTS_OFF = 0, OM_PRIMARY_LISTS_AUTO = 1, OM_PRIMARY_LISTS_ON = 2 };
 om_status om_set_primary_lists(om_ctx* ctx, int32_t mode);
 
-/* Per-kernel-class device time: while enabled, every launch is bracketed by a HIP event
- * pair on its stream (bench.py's roofline uses it).  om_get_kernel_times synchronises
+/* Per-kernel-class device time.  om_set_timing mode 1: every launch is bracketed by a HIP
+ * event pair on its stream; mode 2: the wavefront's bounce-kernel family (bounce 0 ..
+ * tail) of each batch is bracketed once (OM_KT_BOUNCE_SPAN: two events per batch, with
+ * its launch count) — bench.py's roofline uses mode 2.  om_get_kernel_times synchronises
  * the last recorded event, returns the totals since the previous read (or since
  * om_set_timing) and clears them.  Classes: */
 enum {
@@ -233,13 +235,14 @@ enum {
     OM_KT_TAIL = 2,        /* wavefront persistent tail (bounces >= om_set_tail_bounce)   */
     OM_KT_ACCUMULATE = 3,  /* wavefront Stats::add in sample order                          */
     OM_KT_MEGAKERNEL = 4,  /* megakernel pipeline: one launch per render call              */
-    OM_KT_N = 5
+    OM_KT_BOUNCE_SPAN = 5, /* mode 2: bounce 0 .. tail of one batch as one span             */
+    OM_KT_N = 6
 };
 typedef struct om_kernel_times {
     uint64_t launches[OM_KT_N];
     double ms[OM_KT_N];
 } om_kernel_times;
-om_status om_set_timing(om_ctx* ctx, int32_t enable);
+om_status om_set_timing(om_ctx* ctx, int32_t mode);
 om_status om_get_kernel_times(om_ctx* ctx, om_kernel_times* out);
 
 /* ---- display views (draw_to_sdl, main.rs:345-484) ----

@@ -46,13 +46,13 @@ class om_counters(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("samples", "segments", "prim_tests", "pre_tests", "march_steps", "credited")]
 
 
-KT_CLASSES = ("bounce0", "bounce", "tail", "accumulate", "megakernel")   # OM_KT_* order
+KT_CLASSES = ("bounce0", "bounce", "tail", "accumulate", "megakernel", "bounce_span")   # OM_KT_* order
 # draw_to_sdl modes (main.rs:360-367), OM_VIEW_* order
 VIEWS = ("normal", "samples", "sample_blur", "depth", "depth_blur", "ids", "id_blur")
 
 
 class om_kernel_times(C.Structure):
-    _fields_ = [("launches", C.c_uint64 * 5), ("ms", C.c_double * 5)]
+    _fields_ = [("launches", C.c_uint64 * 6), ("ms", C.c_double * 6)]
 
 
 # numpy view of om_pixel_stats (40 B) — render_thread.rs:9-17

@@ -656,14 +656,13 @@ om_status om_set_tail_bounce(om_ctx* c, uint32_t bounce) {
     return OM_OK;
 }
 
-om_status om_set_timing(om_ctx* c, int32_t enable) {
+om_status om_set_timing(om_ctx* c, int32_t mode) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
+    if (mode < 0 || mode > 2) return set_err(c, OM_ERR_INVALID, "om_set_timing: mode must be 0, 1 or 2");
     OM_HIP(c, hipSetDevice(c->device));
-    if (!enable && c->timer.on && !c->timer.cls.empty()) {
-        OM_HIP(c, hipEventSynchronize(c->timer.ev[2 * c->timer.cls.size() - 1]));
-    }
-    c->timer.on = enable != 0;
-    c->timer.cls.clear();
+    if (c->timer.on() && !c->timer.cls.empty()) OM_HIP(c, hipEventSynchronize(c->timer.ev[2 * c->timer.cls.size() - 1]));
+    c->timer.mode = mode;
+    c->timer.clear();
     return OM_OK;
 }
 
@@ -676,10 +675,10 @@ om_status om_get_kernel_times(om_ctx* c, om_kernel_times* out) {
     for (size_t i = 0; i < t.cls.size(); ++i) {
         float ms = 0.0f;
         OM_HIP(c, hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
-        out->launches[t.cls[i]] += 1u;
+        out->launches[t.cls[i]] += t.nl[i];
         out->ms[t.cls[i]] += (double)ms;
     }
-    t.cls.clear();
+    t.clear();
     return OM_OK;
 }
 

@@ -23,28 +23,34 @@ struct Buffers {
     void release();
 };
 
-// Optional per-launch device timing (om_set_timing): a begin/end HIP event pair recorded
-// on the launch stream around every kernel, tagged with its OM_KT_* class.
+// Optional device timing (om_set_timing): HIP event pairs on the launch stream.  Mode 1
+// brackets every launch (tagged with its OM_KT_* class); mode 2 brackets the whole
+// bounce-kernel family of a batch once (OM_KT_BOUNCE_SPAN, with its launch count), which
+// costs two events per batch instead of two per launch.
 struct Timer {
-    bool on = false;
+    int mode = 0;
     std::vector<hipEvent_t> ev;   // pool, pairs (2i, 2i+1)
     std::vector<int> cls;         // class of pair i since the last read
+    std::vector<uint32_t> nl;     // launches inside pair i
+    bool on() const { return mode != 0; }
     void begin(hipStream_t st) {
-        if (!on) return;
+        if (!on()) return;
         const size_t i = 2 * cls.size();
         while (ev.size() < i + 2) {
             hipEvent_t e = nullptr;
-            if (hipEventCreate(&e) != hipSuccess) { on = false; return; }
+            if (hipEventCreate(&e) != hipSuccess) { mode = 0; return; }
             ev.push_back(e);
         }
         (void)hipEventRecord(ev[i], st);
     }
-    void end(int c, hipStream_t st) {
-        if (!on) return;
+    void end(int c, hipStream_t st, uint32_t launches = 1) {
+        if (!on()) return;
         (void)hipEventRecord(ev[2 * cls.size() + 1], st);
         cls.push_back(c);
+        nl.push_back(launches);
     }
-    void release() { for (auto e : ev) (void)hipEventDestroy(e); ev.clear(); cls.clear(); }
+    void clear() { cls.clear(); nl.clear(); }
+    void release() { for (auto e : ev) (void)hipEventDestroy(e); ev.clear(); clear(); }
 };
 
 struct Launch {

@@ -469,27 +469,34 @@ Queue queue(Buffers& B, int k) { return Queue{B.q[k][0], B.q[k][1], B.q[k][2], B
 template <int TR, bool COUNT, bool MARCH>
 void run_batch(Buffers& B, const Launch& L, hipStream_t st, Seg G, const Gen& R, uint32_t depth_cap,
                uint32_t tail_at, uint32_t lds) {
+    Timer& tm = *L.timer;
+    const bool span = tm.mode == 2, each = tm.mode == 1;
+    if (span) tm.begin(st);
+    uint32_t launches = 0;
     for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
         const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
         const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
         if (bounce > 0 && bounce >= tail_at) {
             const uint32_t grid = (G.nseg + kTailSpb - 1u) / kTailSpb;
-            L.timer->begin(st);
+            if (each) tm.begin(st);
             hipLaunchKernelGGL((k_tail<TR, COUNT, MARCH>), dim3(grid), dim3(kBlk), lds, st, L.S, L.P, G, in, cin,
                                B.res, B.res_id, L.counters);
-            L.timer->end(OM_KT_TAIL, st);
+            if (each) tm.end(OM_KT_TAIL, st);
+            if (span) tm.end(OM_KT_BOUNCE_SPAN, st, launches + 1u);
             return;
         }
         uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
-        L.timer->begin(st);
+        if (each) tm.begin(st);
         if (bounce == 0)
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, true>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
                                cin, out, cout, B.res, B.res_id, L.counters);
         else
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
                                cin, out, cout, B.res, B.res_id, L.counters);
-        L.timer->end(bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE, st);
+        if (each) tm.end(bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE, st);
+        ++launches;
     }
+    if (span) tm.end(OM_KT_BOUNCE_SPAN, st, launches);
 }
 
 template <int TR>
@@ -551,14 +558,14 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
             default: run_tr<TR_BVH2_GLOBAL>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
         }
         const uint32_t grid_a = (n_px + kBlk - 1) / kBlk;
-        L.timer->begin(st);
+        if (L.timer->mode == 1) L.timer->begin(st);
         if (L.count)
             hipLaunchKernelGGL(k_accumulate<true>, dim3(grid_a), dim3(kBlk), 0, st, L.P, L.stats, L.pixels, n_px,
                                L.stats_by_pixel ? 1u : 0u, b, B.res, B.res_id, L.S.bloom, L.counters);
         else
             hipLaunchKernelGGL(k_accumulate<false>, dim3(grid_a), dim3(kBlk), 0, st, L.P, L.stats, L.pixels, n_px,
                                L.stats_by_pixel ? 1u : 0u, b, B.res, B.res_id, L.S.bloom, L.counters);
-        L.timer->end(OM_KT_ACCUMULATE, st);
+        if (L.timer->mode == 1) L.timer->end(OM_KT_ACCUMULATE, st);
         if ((e = hipGetLastError()) != hipSuccess) { err = "wavefront launch failed"; return e; }
         done += b;
     }

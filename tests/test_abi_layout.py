@@ -23,7 +23,8 @@ STRUCTS = {
 }
 ENUMS = ["OM_LAMBERTIAN", "OM_METAL", "OM_DIELECTRIC", "OM_KERNEL_AUTO", "OM_KERNEL_BRUTE", "OM_KERNEL_CULLED",
          "OM_KERNEL_BVH", "OM_KERNEL_SBVH", "OM_KERNEL_BVH2", "OM_KERNEL_BVH4", "OM_PIPELINE_MEGAKERNEL", "OM_PIPELINE_WAVEFRONT", "OM_PIPELINE_AUTO",
-         "OM_KT_BOUNCE0", "OM_KT_BOUNCE", "OM_KT_TAIL", "OM_KT_ACCUMULATE", "OM_KT_MEGAKERNEL", "OM_KT_N",
+         "OM_KT_BOUNCE0", "OM_KT_BOUNCE", "OM_KT_TAIL", "OM_KT_ACCUMULATE", "OM_KT_MEGAKERNEL", "OM_KT_BOUNCE_SPAN",
+         "OM_KT_N",
          "OM_OK", "OM_ERR_INVALID", "OM_ERR_DEVICE", "OM_ERR_STATE", "OM_ERR_UNSUPPORTED", "OM_ERR_NOMEM",
          "OM_ABI_VERSION"]
 
