@@ -206,8 +206,9 @@ om_status om_set_counting(om_ctx* ctx, int32_t enable);
  *                          queues in HBM (bounce 0 generates the camera rays), then one
  *                          persistent tail launch, then accumulate
  *   OM_PIPELINE_MEGAKERNEL one persistent-path kernel per call
- *   OM_PIPELINE_AUTO       (default) the faster one measured for the uploaded world:
- *                          megakernel when it has marched primitives, else wavefront */
+ *   OM_PIPELINE_AUTO       (default) the faster one measured for the call: megakernel for
+ *                          worlds with marched primitives and for adaptive renders, else
+ *                          wavefront */
 enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1, OM_PIPELINE_AUTO = 2 };
 om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
 /* Wavefront pipeline: bounces >= `bounce` are finished by one persistent tail launch

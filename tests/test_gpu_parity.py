@@ -198,17 +198,19 @@ def test_auto_pipeline_choice(om, oracle):
     import ctypes as C
     from raytracingoneweekend_amd import _lib as L
     W, H = 24, 16
-    for world, oworld, want in ((om.marched_scene(), oracle.marched_scene(), "megakernel"),
-                                (om.random_scene(0x5EED), oracle.random_scene(0x5EED), "bounce0")):
+    for world, oworld, adaptive, want in ((om.marched_scene(), oracle.marched_scene(), False, "megakernel"),
+                                          (om.random_scene(0x5EED), oracle.random_scene(0x5EED), True, "megakernel"),
+                                          (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, "bounce0")):
         cam = om.default_camera(W / H)
         fz = world.freeze(cam)                                    # pipeline="auto" is the default
         L.check(L.lib.om_set_timing(fz.ctx, 1), fz.ctx)
         pix = om.PixelsBox.new(W * H)
-        om.render(cam, fz, 50, 0.001, 100.0, 2, W, H, pix, seed=8, march_steps=256)
+        om.render(cam, fz, 50, 0.001, 100.0, 8, W, H, pix, seed=8, march_steps=256, adaptive=adaptive)
         kt = L.om_kernel_times()
         L.check(L.lib.om_get_kernel_times(fz.ctx, C.byref(kt)), fz.ctx)
         assert kt.launches[L.KT_CLASSES.index(want)] > 0, want
-        exp, _ = oracle.render(oworld, oracle.default_camera(W / H), oracle.params(W, H, 2, seed=8, march_steps=256))
+        exp, _ = oracle.render(oworld, oracle.default_camera(W / H),
+                               oracle.params(W, H, 8, seed=8, march_steps=256, adaptive=adaptive))
         nb, msg = compare_stats(pix.pixels, exp, f"auto/{want}")
         assert nb == 0, msg
 
