@@ -40,7 +40,8 @@ constexpr int kBlock = 256;
 // ---------------------------------------------------------------------------
 // closest hit over the traced primitives
 // ---------------------------------------------------------------------------
-enum { MODE_BRUTE = 1, MODE_CULLED = 2, MODE_BVH = 3, MODE_SBVH_LDS = 4, MODE_SBVH_GLOBAL = 5 };
+enum { MODE_BRUTE = 1, MODE_CULLED = 2, MODE_BVH = 3, MODE_SBVH_LDS = 4, MODE_SBVH_GLOBAL = 5, MODE_BVH2 = 6 };
+constexpr int kStack2 = 24;                    // BVH2 lane-stack bound (om_upload_world checks the depth)
 constexpr int kBlockLds = 512;
 constexpr uint32_t kLdsBudget = 96u * 1024u;   // staged scene per workgroup (160 KiB per CU)
 
@@ -58,7 +59,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 
 extern __shared__ __attribute__((aligned(16))) uint4 om_lds[];
 
-template <int MODE, int BLOCK, bool COUNT>
+// MARCH is a compile-time split (as in the wavefront): traced-only scenes do not carry
+// the sphere-tracing code's registers.
+template <int MODE, int BLOCK, bool COUNT, bool MARCH>
 __global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(OmSceneDev S, OmCamDev C, OmParamsDev P,
                                                        const float2* __restrict__ jitter,
                                                        om_pixel_stats* __restrict__ stats,
@@ -75,6 +78,21 @@ __global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(O
     }
     const OmSkipNode* lds_nodes = (const OmSkipNode*)om_lds;
     const OmAffineTest* lds_recs = (const OmAffineTest*)(om_lds + S.n_snodes * 2u);
+    // BVH2: [lane stack][nodes][leaf table] in LDS (nodes through L2 when they exceed the budget)
+    uint16_t* b2_stk = (uint16_t*)om_lds + threadIdx.x;
+    const OmBvh2Node* b2_nodes = S.b2nodes;
+    const uint32_t* b2_leaves = S.b2leaves;
+    if (MODE == MODE_BVH2 && S.b2_lds_bytes) {
+        uint4* dst = om_lds + (BLOCK * S.b2_stack * 2u) / 16u;
+        const uint32_t nn = S.n_b2nodes * 4u;
+        const uint4* sn = (const uint4*)S.b2nodes;
+        for (uint32_t i = threadIdx.x; i < nn; i += BLOCK) dst[i] = sn[i];
+        uint32_t* ldst = (uint32_t*)(dst + nn);
+        for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += BLOCK) ldst[i] = S.b2leaves[i];
+        __syncthreads();
+        b2_nodes = (const OmBvh2Node*)dst;
+        b2_leaves = ldst;
+    }
     const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
     uint32_t pixel, slot;
     bool valid;
@@ -102,7 +120,6 @@ __global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(O
     const uint32_t line = valid ? pixel / P.width : 0u;
     const float j_f = (float)line, i_f = (float)(pixel - P.width * line);
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
-    const bool has_marched = (S.n_msph + S.n_mbox + S.n_mtor) != 0u;
 
     uint32_t todo = valid ? P.sample_count : 0u;
     bool live = false;
@@ -154,8 +171,9 @@ __global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(O
         if (MODE == MODE_SBVH_LDS) best = traced_sbvh(S, lds_nodes, lds_recs, o, d, P.tmin, closest, w);
         else if (MODE == MODE_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
         else if (MODE == MODE_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
+        else if (MODE == MODE_BVH2) best = traced_bvh2<kStack2, BLOCK>(S, b2_nodes, b2_leaves, S.srecs, b2_stk, o, d, P.tmin, closest, w);
         else best = traced_brute<MODE == MODE_CULLED>(S, o, d, P.tmin, closest, w);
-        if (has_marched) {
+        if (MARCH) {
             float tm;
             const int mg = march(S, o, d, P.tmin, P.tmax, closest, P.march_steps, tm, w);
             if (mg >= 0) { best = mg; closest = tm; }
@@ -344,10 +362,15 @@ template <int MODE, int BLOCK>
 void go(bool count, uint64_t threads, uint32_t lds, hipStream_t stream, const OmSceneDev& S, const OmCamDev& C,
         const OmParamsDev& P, const float2* jt, om_pixel_stats* st, const uint32_t* px, unsigned long long* ctr) {
     const uint32_t blocks = (uint32_t)((threads + BLOCK - 1) / BLOCK);
-    if (count)
-        hipLaunchKernelGGL((render_kernel<MODE, BLOCK, true>), dim3(blocks), dim3(BLOCK), lds, stream, S, C, P, jt, st, px, ctr);
+    const bool march = (S.n_msph + S.n_mbox + S.n_mtor) != 0u;
+    if (count && march)
+        hipLaunchKernelGGL((render_kernel<MODE, BLOCK, true, true>), dim3(blocks), dim3(BLOCK), lds, stream, S, C, P, jt, st, px, ctr);
+    else if (count)
+        hipLaunchKernelGGL((render_kernel<MODE, BLOCK, true, false>), dim3(blocks), dim3(BLOCK), lds, stream, S, C, P, jt, st, px, ctr);
+    else if (march)
+        hipLaunchKernelGGL((render_kernel<MODE, BLOCK, false, true>), dim3(blocks), dim3(BLOCK), lds, stream, S, C, P, jt, st, px, ctr);
     else
-        hipLaunchKernelGGL((render_kernel<MODE, BLOCK, false>), dim3(blocks), dim3(BLOCK), lds, stream, S, C, P, jt, st, px, ctr);
+        hipLaunchKernelGGL((render_kernel<MODE, BLOCK, false, false>), dim3(blocks), dim3(BLOCK), lds, stream, S, C, P, jt, st, px, ctr);
 }
 
 // Primary-ray candidate lists for (camera, frame, world), rebuilt only when one changes.
@@ -425,7 +448,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         pipeline = ((c->scene.n_msph + c->scene.n_mbox + c->scene.n_mtor) || p->adaptive) ? OM_PIPELINE_MEGAKERNEL
                                                                                           : OM_PIPELINE_WAVEFRONT;
     int mode = c->kernel;
-    if (mode == OM_KERNEL_AUTO) mode = pipeline == OM_PIPELINE_WAVEFRONT ? OM_KERNEL_BVH2 : OM_KERNEL_BVH;
+    if (mode == OM_KERNEL_AUTO) mode = OM_KERNEL_BVH2;
     if (pipeline == OM_PIPELINE_WAVEFRONT) {
         omw::Launch L;
         L.S = c->scene; L.C = C; L.P = P;
@@ -481,6 +504,9 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         go<MODE_BRUTE, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
     } else if (mode == OM_KERNEL_CULLED) {
         go<MODE_CULLED, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
+    } else if ((mode == OM_KERNEL_BVH2 || mode == OM_KERNEL_BVH4) && c->scene.n_b2nodes) {
+        const uint32_t lds = kBlock * c->scene.b2_stack * 2u + c->scene.b2_lds_bytes;
+        go<MODE_BVH2, kBlock>(count, threads, lds, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
     } else {
         go<MODE_BVH, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
     }
