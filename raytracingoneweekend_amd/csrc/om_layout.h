@@ -58,7 +58,7 @@ struct OM_ALIGN16 OmMBox {
     float center[3];
     float pad0;
     float sizes[3];
-    float pad1;
+    float br;         // march cull: upper bound of |sizes| (the box lies within |p - center| <= |sizes|)
 };
 // MarchedTorus (marched.rs:105-113)
 struct OM_ALIGN16 OmMTorus {
@@ -68,6 +68,13 @@ struct OM_ALIGN16 OmMTorus {
     float w2l_s[4];
     float sizes[3];
     float min_scale;  // l2w_s.xyz().min_val() (marched.rs:148-150), precomputed
+    // conservative cull of the SDF evaluation (march): |sdf(p)| >= |p - bc| / bk - br,
+    // all with margins, so a step skips the torus when that bound already exceeds the
+    // running minimum
+    float bc[3];      // world centre: translation of l2w_tr scaled by l2w_s
+    float bk;         // upper bound of (max scale) / min_scale-margined factor (see om_world.cpp)
+    float br;         // upper bound of (R + r) / min-w2l_s factor
+    float pad_b[3];
 };
 // Material (materials.rs:18-24), padded to 32 B.
 struct OM_ALIGN16 OmMaterial {

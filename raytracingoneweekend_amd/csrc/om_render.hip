@@ -442,8 +442,8 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     if (threads == 0) return OM_OK;
     int pipeline = c->pipeline;
     // AUTO: the measured faster pipeline: the megakernel for marched SDFs (C2:
-    // 741 vs 555 Msamples/s) and for adaptive sampling (one sample per pixel per wavefront
-    // pass; C1 adaptive: 1964 vs 554 credited Msamples/s), else the wavefront.
+    // 916 vs 790 Msamples/s) and for adaptive sampling (one sample per pixel per wavefront
+    // pass; C1 adaptive: 2804 vs 553 credited Msamples/s), else the wavefront.
     if (pipeline == OM_PIPELINE_AUTO)
         pipeline = ((c->scene.n_msph + c->scene.n_mbox + c->scene.n_mtor) || p->adaptive) ? OM_PIPELINE_MEGAKERNEL
                                                                                           : OM_PIPELINE_WAVEFRONT;

@@ -245,8 +245,23 @@ __device__ __forceinline__ int march(const OmSceneDev& S, F3 o, F3 d, float tmin
         p = at(o, d, t);
         float best = INFINITY; int bk = -1; uint32_t bi = 0;
         for (uint32_t i = 0; i < S.n_msph; ++i) { const float v = fabsf(msphere_sdf(S.msph[i], p)); if (v < best) { best = v; bk = 0; bi = i; } }
-        for (uint32_t i = 0; i < S.n_mbox; ++i) { const float v = fabsf(mbox_sdf(S.mbox[i], p)); if (v < best) { best = v; bk = 1; bi = i; } }
-        for (uint32_t i = 0; i < S.n_mtor; ++i) { const float v = fabsf(mtorus_sdf(S.mtor[i], p)); if (v < best) { best = v; bk = 2; bi = i; } }
+        for (uint32_t i = 0; i < S.n_mbox; ++i) {
+            const OmMBox& B = S.mbox[i];
+            const float dx = p.x - B.center[0], dy = p.y - B.center[1], dz = p.z - B.center[2];
+            const float thr = (best + B.br) * 1.0001f;                         // inf/NaN -> evaluate
+            if (dx * dx + dy * dy + dz * dz > thr * thr) continue;
+            const float v = fabsf(mbox_sdf(B, p));
+            if (v < best) { best = v; bk = 1; bi = i; }
+        }
+        for (uint32_t i = 0; i < S.n_mtor; ++i) {
+            const OmMTorus& T = S.mtor[i];
+            // conservative cull (om_world.cpp): |sdf| provably > best -> it cannot be the new minimum
+            const float dx = p.x - T.bc[0], dy = p.y - T.bc[1], dz = p.z - T.bc[2];
+            const float thr = best * T.bk + T.br;                              // inf/NaN -> evaluate
+            if (dx * dx + dy * dy + dz * dz > thr * thr) continue;
+            const float v = fabsf(mtorus_sdf(T, p));
+            if (v < best) { best = v; bk = 2; bi = i; }
+        }
         if (bk < 0) return -1;                                                 // hits.rs:323
         if (best < HIT) {                                                      // hits.rs:325-327
             t_hit = t;

@@ -216,7 +216,12 @@ void om_world::freeze(FrozenWorld& fw) const {
     }
     fw.mbox.resize(mbox.size());
     for (size_t i = 0; i < mbox.size(); ++i) {
-        mbox[i].center.store(fw.mbox[i].center); mbox[i].sizes.store(fw.mbox[i].sizes); fw.mbox[i].pad0 = fw.mbox[i].pad1 = 0.0f;
+        mbox[i].center.store(fw.mbox[i].center); mbox[i].sizes.store(fw.mbox[i].sizes); fw.mbox[i].pad0 = 0.0f;
+        {   // |sdf| >= |p - center| - |sizes| (margins: f32 rounding of the SDF and of the test)
+            const double sx = mbox[i].sizes.e[0], sy = mbox[i].sizes.e[1], sz = mbox[i].sizes.e[2];
+            const double hd = std::sqrt(sx * sx + sy * sy + sz * sz);
+            fw.mbox[i].br = std::isfinite(hd) ? (float)(hd * (1.0 + 1e-4) + 1e-4) : NAN;
+        }
         put_mat(fw.offsets[K_MBOX] + (uint32_t)i, mbox[i].mat);
     }
     fw.mtor.resize(mtor.size());
@@ -226,6 +231,20 @@ void om_world::freeze(FrozenWorld& fw) const {
         for (int k = 0; k < 4; ++k) { o.l2w_s[k] = t.l2w_s.e[k]; o.w2l_s[k] = t.w2l_s.e[k]; }
         t.sizes.store(o.sizes);
         o.min_scale = std::fmin(t.l2w_s.e[0], std::fmin(t.l2w_s.e[1], t.l2w_s.e[2]));     // Vec3::min_val vec3.rs:50-52
+        // march cull: q = W2L_TR (p * w2l_s) with W2L_TR rigid, so |q| = |p * w2l_s - d|
+        // >= |p - d * l2w_s| * min(w2l_s), and the torus lies within |q| <= R + r:
+        // |sdf| >= (|p - bc| * kq - (R + r)) * min_scale.  A step skips the torus when
+        // |p - bc| > (best / min_scale + R + r) / kq, i.e. |p - bc|^2 > (best * bk + br)^2.
+        {
+            const double kq = std::min({(double)t.w2l_s.e[0], (double)t.w2l_s.e[1], (double)t.w2l_s.e[2]}) * (1.0 - 1e-4);
+            const double ms = (double)o.min_scale * (1.0 - 1e-4);
+            const double rr = std::fabs((double)t.sizes.e[0]) + std::fabs((double)t.sizes.e[1]);
+            const bool ok = kq > 0.0 && ms > 0.0 && std::isfinite(kq) && std::isfinite(ms) && std::isfinite(rr);
+            for (int k = 0; k < 3; ++k) o.bc[k] = (float)((double)t.l2w_tr.r[k].e[3] * (double)t.l2w_s.e[k]);
+            o.bk = ok ? (float)(1.0 / (ms * kq) * (1.0 + 1e-4)) : NAN;          // NaN: never cull
+            o.br = ok ? (float)((rr * (1.0 + 1e-4) + 1e-4) / kq * (1.0 + 1e-4)) : NAN;
+            o.pad_b[0] = o.pad_b[1] = o.pad_b[2] = 0.0f;
+        }
         put_mat(fw.offsets[K_MTORUS] + (uint32_t)i, t.mat);
     }
     build_bvh(*this, fw);
