@@ -109,6 +109,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, the measured path); gloo gathers through host memory and maps "
                          "ranks onto the visible GPUs (a functional rehearsal of N>1 on a 1-GPU box)")
+    ap.add_argument("--primary-lists", default="auto", choices=["off", "auto", "on"],
+                    help="bounce-0 per-tile candidate lists (DESIGN.md §5.10); auto = when they average <= 12")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
@@ -142,6 +144,7 @@ def main():
     frozen = world.freeze(cam, device=local_rank, kernel=args.kernel, pipeline=args.pipeline)
     ctx = frozen.ctx
     L.check(L.lib.om_set_tail_bounce(ctx, args.tail), ctx)
+    L.check(L.lib.om_set_primary_lists(ctx, {"off": 0, "auto": 1, "on": 2}[args.primary_lists]), ctx)
     spp_step = SPP_PER_STEP * world_size                     # fixed per-GPU samples per step
     spp_total = spp_step * args.steps
     pix = shard.tile_pixels(W, H, rank, world_size)

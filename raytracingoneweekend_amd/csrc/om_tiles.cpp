@@ -8,9 +8,10 @@
 // ((llc - O).n) / ((X - O).n) with n = H x V.  So over the lens the projection of X moves
 // by at most R |1 - s| in the focus plane.  For a box in front of the camera the
 // projection from O is the hull of the corner projections and |1 - s| peaks at a corner,
-// which bounds the (u, v) footprint of every ray that can touch the box.  Boxes
-// reaching behind the camera plane go to every tile.  Everything is evaluated in double
-// with a 3-pixel margin, far beyond the f32 rounding of the kernel's ray set-up.
+// which bounds the (u, v) footprint of every ray that can touch the box.  Boxes wholly
+// behind the lens plane are never reached; boxes straddling it go to every tile.
+// Everything is evaluated in double with a 3-pixel margin, far beyond the f32 rounding
+// of the kernel's ray set-up.
 #include "om_tiles.h"
 
 #include <algorithm>
@@ -50,6 +51,18 @@ bool build(const std::vector<float>& srec_box, const om_camera& cam, uint32_t W,
         const float* b = &srec_box[6 * r];
         double a0 = INFINITY, a1 = -INFINITY, b0 = INFINITY, b1 = -INFINITY, k = 0.0;
         bool all = false;
+        // a box wholly behind the lens plane (through O, normal n; every lens point lies on
+        // it) is never reached: a ray's points X = L + t (P - L), t >= tmin > 0, have
+        // (X - O).n of num's sign.  Margin: 1e-6 relative + 1e-4 world units (f32 origins).
+        int behind = 0;
+        const double nl = std::sqrt(dot(n, n));
+        for (int c = 0; c < 8; ++c) {
+            const D3 X{(c & 1) ? b[3] : b[0], (c & 2) ? b[4] : b[1], (c & 4) ? b[5] : b[2]};
+            const D3 dX = sub(X, O);
+            const double ahead = dot(dX, n) / nl * (num > 0 ? 1.0 : -1.0);     // signed distance in front
+            behind += ahead < -(1e-6 * std::sqrt(dot(dX, dX)) + 1e-4) ? 1 : 0;
+        }
+        if (behind == 8) { rect[r] = Rect{1u, 0u, 1u, 0u}; continue; }
         for (int c = 0; c < 8 && !all; ++c) {
             const D3 X{(c & 1) ? b[3] : b[0], (c & 2) ? b[4] : b[1], (c & 4) ? b[5] : b[2]};
             const D3 dX = sub(X, O);
