@@ -40,7 +40,7 @@ def main():
            "hbm_bytes_per_launch": round(2.0 * fetch + write),
            "fetch_bytes_x2_per_launch": round(2.0 * fetch), "write_bytes_per_launch": round(write),
            "dispatches": {"FETCH_SIZE": nf, "WRITE_SIZE": nw},
-           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/pmc.sh), {os.path.basename(tag)}; "
+           "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes (tools/pmc.sh), {os.path.relpath(os.path.abspath(tag), os.path.abspath('gpurun_out'))}; "
                      "FETCH_SIZE x2 (gfx950)"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res))
