@@ -4,8 +4,9 @@ Workload (config C1, BASELINE.json configs[1]): the S-traced random_scene (main.
 minus the torus block, om-rng scene seed 0x5EED), camera of main.rs:136-142, 1920x1080,
 max_depth 50, tmin 0.001, tmax 100, fixed spp (adaptive off).  One STEP = one progressive
 pass of SPP_PER_STEP samples over every pixel this rank owns, accumulated into the
-per-pixel Stats in HBM (render_thread.rs:176-199, batched).  32 steps at N=1 = the full
-512-spp frame.
+per-pixel Stats in HBM (render_thread.rs:176-199, batched).  16 steps of 32 spp at N=1 =
+the full 512-spp frame; the library runs each step as two concurrent 16-spp batches
+(om_set_streams).
 
 N>1 (torch.distributed.run, one rank per GPU): 8x8 pixel tiles are dealt round-robin to
 ranks (main.rs:172-189's chunk round-robin); every rank renders its tiles at
@@ -33,7 +34,7 @@ from raytracingoneweekend_amd import _lib as L  # noqa: E402
 from raytracingoneweekend_amd import shard  # noqa: E402
 
 W, H, MAX_DEPTH, TMIN, TMAX, SEED, SCENE_SEED = 1920, 1080, 50, 0.001, 100.0, 1, 0x5EED
-SPP_PER_STEP = 16
+SPP_PER_STEP = 32
 # BASELINE.json configs: C1 is the metric's workload (the default line); C2/C3 are measured
 # with --config for DESIGN.md (the marched SDF scene at 256 march steps, the 10k-sphere BVH).
 CONFIGS = {
@@ -98,11 +99,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", default="C1", choices=list(CONFIGS))
-    ap.add_argument("--steps", type=int, default=None, help="default: the config's spp / 16 (C1: 32)")
+    ap.add_argument("--steps", type=int, default=None, help="default: the config's spp / spp-per-step (C1: 32)")
+    ap.add_argument("--spp-per-step", type=int, default=SPP_PER_STEP, help="samples per pixel per step (one render call)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
     ap.add_argument("--pipeline", default="auto", choices=list(L.PIPELINES))
     ap.add_argument("--tail", type=int, default=0, help="first bounce of the persistent tail launch (0 = library default)")
+    ap.add_argument("--streams", type=int, default=2, help="wavefront batches in flight per call (om_set_streams; 1 = serial)")
     ap.add_argument("--kernel-timing", default="span", choices=["span", "launch", "off"],
                     help="HIP events in the timed region: span = once around each batch's bounce kernels "
                          "(2 events/step, default), launch = around every launch (per-kernel breakdown)")
@@ -116,7 +119,7 @@ def main():
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     if args.steps is None:
-        args.steps = cfg["spp"] // SPP_PER_STEP
+        args.steps = cfg["spp"] // args.spp_per_step
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -144,8 +147,9 @@ def main():
     frozen = world.freeze(cam, device=local_rank, kernel=args.kernel, pipeline=args.pipeline)
     ctx = frozen.ctx
     L.check(L.lib.om_set_tail_bounce(ctx, args.tail), ctx)
+    L.check(L.lib.om_set_streams(ctx, args.streams), ctx)
     L.check(L.lib.om_set_primary_lists(ctx, {"off": 0, "auto": 1, "on": 2}[args.primary_lists]), ctx)
-    spp_step = SPP_PER_STEP * world_size                     # fixed per-GPU samples per step
+    spp_step = args.spp_per_step * world_size                # fixed per-GPU samples per step
     spp_total = spp_step * args.steps
     pix = shard.tile_pixels(W, H, rank, world_size)
     n_px = int(pix.size)
@@ -203,7 +207,24 @@ def main():
     host = stats.cpu().numpy().view(L.PIXEL_STATS_DTYPE).copy()
     assert int(host["n"].min()) == spp_total and int(host["n"].max()) == spp_total, "every pixel must take every sample"
 
-    # work counting (untimed): the same K launches again with the counting build; the
+    # per-launch durations (untimed): the same K steps again, production build, every launch
+    # bracketed by events on its stream (om_set_timing 1) -> the rocprof-comparable average
+    # launch duration and the launch concurrency inside a call; same frame, bit for bit
+    mega = kt.launches[L.KT_CLASSES.index("megakernel")] > 0     # the pipeline that actually ran (auto)
+    fam = [L.KT_CLASSES.index("megakernel")] if mega else [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
+    span_i = L.KT_CLASSES.index("megakernel" if mega else "bounce_span")
+    kl = L.om_kernel_times()
+    if timing:
+        stats.zero_()
+        L.check(L.lib.om_set_timing(ctx, 1), ctx)
+        for _ in range(args.steps):
+            step(p)
+        torch.cuda.synchronize()
+        L.check(L.lib.om_get_kernel_times(ctx, C.byref(kl)), ctx)
+        L.check(L.lib.om_set_timing(ctx, 0), ctx)
+        assert np.array_equal(stats.cpu().numpy(), host.view(np.uint8)), "per-launch timing changed the result"
+
+    # work counting (untimed): the same K steps again with the counting build; the
     # frame it produces must equal the timed one bit for bit (counters change nothing)
     stats.zero_()
     L.check(L.lib.om_reset_counters(ctx, sptr), ctx)
@@ -219,23 +240,19 @@ def main():
     value = total_samples / elapsed / 1e6
 
     # roofline of the dominant kernel: the fused trace+shade bounce kernel (all its launches:
-    # bounce 0, bounces 1.., tail), algorithmic flops from the live counters / its event time
-    mega = kt.launches[L.KT_CLASSES.index("megakernel")] > 0     # the pipeline that actually ran (auto)
-    if mega:
-        fam = [L.KT_CLASSES.index("megakernel")]
-    elif args.kernel_timing == "span":
-        fam = [L.KT_CLASSES.index("bounce_span")]
-    else:
-        fam = [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
-    launches = sum(kt.launches[i] for i in fam)
-    kern_s = sum(kt.ms[i] for i in fam) / 1e3
+    # bounce 0, bounces 1.., tail), algorithmic flops from the live counters.  Its launches run
+    # two at a time (concurrent batches), so the rate is the family's flops over the time it
+    # holds the GPU: the timed region's call spans (events on the call's stream).
+    launches = sum(kl.launches[i] for i in fam) if timing else 0
     roof = None
     if timing and launches:
+        span_s = kt.ms[span_i] / 1e3                               # timed region: the calls' device time
+        per_launch_s = sum(kl.ms[i] for i in fam) / 1e3 / launches  # rerun: mean launch duration
+        rerun_span_s = kl.ms[span_i] / 1e3
         flops = (FLOP_EXACT_TEST * ctr.prim_tests + FLOP_BOX_TEST * ctr.pre_tests + FLOP_SEGMENT * ctr.segments
                  + FLOP_CAMERA_RAY * ctr.samples + FLOP_MARCH_STEP * ctr.march_steps)
         nbytes = BYTES_PER_LATER_SEGMENT * (ctr.segments - ctr.samples) + BYTES_PER_SAMPLE * ctr.samples
-        avg_launch_s = kern_s / launches
-        achieved_tflops = flops / kern_s / 1e12
+        achieved_tflops = flops / span_s / 1e12
         traffic, traffic_src = None, None
         if os.path.exists(PMC_TRAFFIC) and not mega and args.kernel == "auto" and args.config == "C1":
             pm = json.load(open(PMC_TRAFFIC))
@@ -243,12 +260,15 @@ def main():
         roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": traffic,
                 "kernel": "render_kernel (megakernel)" if mega else "k_bounce0+k_bounce+k_tail (fused trace+shade)",
-                "launches_per_step": round(launches / args.steps, 2), "avg_launch_ms": round(avg_launch_s * 1e3, 4),
+                "launches_per_step": round(launches / args.steps, 2),
+                "avg_launch_ms": round(per_launch_s * 1e3, 4),
+                "effective_ms_per_launch": round(span_s / launches * 1e3, 4),
+                "launch_concurrency": round(per_launch_s * launches / rerun_span_s, 3) if rerun_span_s else None,
                 "flop_per_launch": round(flops / launches), "algorithmic_bytes_per_launch": round(nbytes / launches),
-                "hbm_achieved_gbs": round(nbytes / kern_s / 1e9, 2), "traffic_source": traffic_src,
-                "kernel_share_of_step": round(kern_s / elapsed, 4), "timing": args.kernel_timing,
-                "all_kernels_ms_per_step": {k: round(kt.ms[i] / args.steps, 4) for i, k in enumerate(L.KT_CLASSES)
-                                            if kt.launches[i]}}
+                "hbm_achieved_gbs": round(nbytes / span_s / 1e9, 2), "traffic_source": traffic_src,
+                "kernel_share_of_step": round(span_s / elapsed, 4), "timing": args.kernel_timing,
+                "all_kernels_ms_per_step": {k: round(kl.ms[i] / args.steps, 4) for i, k in enumerate(L.KT_CLASSES)
+                                            if kl.launches[i]}}
     hbm_gbs = roof["hbm_achieved_gbs"] if roof else None
 
     if rank == 0:
@@ -277,7 +297,7 @@ def main():
                        "parallelism": f"tile{world_size}" + ("/gloo" if gloo and world_size > 1 else ""),
                        "kernel": args.kernel,
                        "pipeline": args.pipeline + (("->megakernel" if mega else "->wavefront") if args.pipeline == "auto" else ""),
-                       "tail_bounce": args.tail or "default"},
+                       "tail_bounce": args.tail or "default", "streams": args.streams},
             "hbm_gbs": hbm_gbs,
             "roofline": roof,
             "work": {"segments_per_sample": round(ctr.segments / max(1, ctr.samples), 4),

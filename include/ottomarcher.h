@@ -215,6 +215,14 @@ om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
  * scheduling knob: results are bit-identical for every value. */
 om_status om_set_tail_bounce(om_ctx* ctx, uint32_t bounce);
 
+/* Wavefront, fixed-spp calls: batches in flight (1..4; default 2).  The call's samples are
+ * split into batches of at most 1/streams of the call, dealt round-robin to `streams` HIP
+ * streams (the call's stream plus context-owned side streams), each with its own queue set;
+ * one batch's latency-bound phases (launch drains, late bounces, tail) then run beside the
+ * other's full ones.  Accumulation stays in sample order and the call ends joined on its
+ * stream, so results are bit-identical for every value.  1 = one batch after another. */
+om_status om_set_streams(om_ctx* ctx, uint32_t streams);
+
 /* Primary rays (wavefront, BVH2): bounce 0 can test, per 8x8 pixel tile, only the leaf
  * records a conservative lens-aware frustum of the tile reaches, instead of traversing
  * the BVH (the conservative form of the reference's camera hash, camera_hash.rs;
@@ -224,18 +232,19 @@ enum { OM_PRIMARY_LISTS_OFF = 0, OM_PRIMARY_LISTS_AUTO = 1, OM_PRIMARY_LISTS_ON 
 om_status om_set_primary_lists(om_ctx* ctx, int32_t mode);
 
 /* Per-kernel-class device time.  om_set_timing mode 1: every launch is bracketed by a HIP
- * event pair on its stream; mode 2: the wavefront's bounce-kernel family (bounce 0 ..
- * tail) of each batch is bracketed once (OM_KT_BOUNCE_SPAN: two events per batch, with
- * its launch count) — bench.py's roofline uses mode 2.  om_get_kernel_times synchronises
- * the last recorded event, returns the totals since the previous read (or since
- * om_set_timing) and clears them.  Classes: */
+ * event pair on its stream, and each wavefront call as a whole; mode 2: only each wavefront
+ * call (OM_KT_BOUNCE_SPAN: two events per call on the call's stream, counting the call's
+ * bounce-family launches; with concurrent batches, launches overlap inside it) — bench.py's
+ * roofline uses mode 2 in the timed region and mode 1 in an untimed rerun.
+ * om_get_kernel_times synchronises the recorded events, returns the totals since the
+ * previous read (or since om_set_timing) and clears them.  Classes: */
 enum {
     OM_KT_BOUNCE0 = 0,     /* wavefront bounce 0: camera rays + trace + shade + compact   */
     OM_KT_BOUNCE = 1,      /* wavefront bounce b >= 1: trace + shade + compact              */
     OM_KT_TAIL = 2,        /* wavefront persistent tail (bounces >= om_set_tail_bounce)   */
     OM_KT_ACCUMULATE = 3,  /* wavefront Stats::add in sample order                          */
     OM_KT_MEGAKERNEL = 4,  /* megakernel pipeline: one launch per render call              */
-    OM_KT_BOUNCE_SPAN = 5, /* mode 2: bounce 0 .. tail of one batch as one span             */
+    OM_KT_BOUNCE_SPAN = 5, /* one wavefront call: snapshot .. last accumulate (all batches)   */
     OM_KT_N = 6
 };
 typedef struct om_kernel_times {

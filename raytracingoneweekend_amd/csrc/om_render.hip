@@ -264,6 +264,7 @@ struct om_ctx {
     bool count_work = true;
     int pipeline = OM_PIPELINE_AUTO;
     uint32_t tail_bounce = 0;
+    uint32_t wf_streams = 2;            // wavefront fixed-spp calls: batches in flight (om_set_streams)
     // primary-ray tile lists (om_tiles.h): host record boxes of the uploaded world, the
     // device lists of the last (camera, frame, world) and the policy (om_set_primary_lists)
     std::vector<float> srec_box;
@@ -457,6 +458,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         L.counters = (unsigned long long*)c->counters.p;
         L.count = c->count_work;
         L.tail_bounce = c->tail_bounce;
+        L.streams = c->wf_streams;
         L.timer = &c->timer;
         L.tile_off = nullptr; L.tile_idx = nullptr;
         if (mode == OM_KERNEL_BVH2 && c->scene.n_b2nodes) {
@@ -494,7 +496,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     const float2* jt = (const float2*)c->jitter.p;
     unsigned long long* ctr = (unsigned long long*)c->counters.p;
     const bool count = c->count_work;
-    c->timer.begin(stream);
+    const int mk_ti = c->timer.begin(stream);
     if (mode == OM_KERNEL_SBVH) {
         if (c->scene.lds_bytes)
             go<MODE_SBVH_LDS, kBlockLds>(count, threads, c->scene.lds_bytes, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
@@ -510,7 +512,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     } else {
         go<MODE_BVH, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
     }
-    c->timer.end(OM_KT_MEGAKERNEL, stream);
+    c->timer.end(mk_ti, OM_KT_MEGAKERNEL, stream);
     OM_HIP(c, hipGetLastError());
     return OM_OK;
 }
@@ -686,11 +688,19 @@ om_status om_set_tail_bounce(om_ctx* c, uint32_t bounce) {
     return OM_OK;
 }
 
+om_status om_set_streams(om_ctx* c, uint32_t streams) {
+    if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
+    if (streams < 1 || streams > (uint32_t)omw::kMaxSets) return set_err(c, OM_ERR_INVALID, "om_set_streams: streams must be 1..4");
+    c->wf_streams = streams;
+    return OM_OK;
+}
+
 om_status om_set_timing(om_ctx* c, int32_t mode) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
     if (mode < 0 || mode > 2) return set_err(c, OM_ERR_INVALID, "om_set_timing: mode must be 0, 1 or 2");
     OM_HIP(c, hipSetDevice(c->device));
-    if (c->timer.on() && !c->timer.cls.empty()) OM_HIP(c, hipEventSynchronize(c->timer.ev[2 * c->timer.cls.size() - 1]));
+    for (size_t i = 0; c->timer.on() && i < c->timer.cls.size(); ++i)
+        if (c->timer.cls[i] >= 0) OM_HIP(c, hipEventSynchronize(c->timer.ev[2 * i + 1]));
     c->timer.mode = mode;
     c->timer.clear();
     return OM_OK;
@@ -701,8 +711,9 @@ om_status om_get_kernel_times(om_ctx* c, om_kernel_times* out) {
     OM_HIP(c, hipSetDevice(c->device));
     *out = om_kernel_times{};
     omw::Timer& t = c->timer;
-    if (!t.cls.empty()) OM_HIP(c, hipEventSynchronize(t.ev[2 * t.cls.size() - 1]));
     for (size_t i = 0; i < t.cls.size(); ++i) {
+        if (t.cls[i] < 0) continue;
+        OM_HIP(c, hipEventSynchronize(t.ev[2 * i + 1]));
         float ms = 0.0f;
         OM_HIP(c, hipEventElapsedTime(&ms, t.ev[2 * i], t.ev[2 * i + 1]));
         out->launches[t.cls[i]] += t.nl[i];

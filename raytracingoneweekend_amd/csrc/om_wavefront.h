@@ -11,43 +11,60 @@
 
 namespace omw {
 
-// Device work buffers of one context; grown on demand, never shrunk.
-struct Buffers {
-    uint64_t cap = 0;            // paths per batch
+// One batch's device work buffers: ping-pong path queues, result slots, per-bounce counts.
+struct QueueSet {
     float4* q[2][3] = {{nullptr, nullptr, nullptr}, {nullptr, nullptr, nullptr}};  // ping-pong queues: o|depthf, d|first_id, cur|seg
     uint4* qr[2] = {nullptr, nullptr};   // rng lo, rng hi, path slot, pad
     float4* res = nullptr;       // colour.xyz, depth
     uint32_t* res_id = nullptr;  // obj id (0xFFFFFFFF = no sample)
     uint32_t* counts = nullptr;  // per bounce, per queue segment: live rays
-    uint32_t counts_n = 0;       // words allocated
+    void release();
+};
+
+// Device work buffers of one context; grown on demand, never shrunk.  kMaxSets queue sets
+// let that many batches be in flight at once (overlapped schedule): batch
+// i uses set i % S on stream i % S (stream 0 = the caller's stream, the others `side`).
+constexpr int kMaxSets = 4;
+struct Buffers {
+    uint64_t cap = 0;            // paths per batch (per set)
+    uint32_t counts_n = 0;       // count words per set
+    int nsets = 0;               // sets allocated at `cap`
+    QueueSet set[kMaxSets];
+    uint32_t* n0 = nullptr;      // per listed pixel: Stats.n at the start of the call
+    uint64_t n0_cap = 0;
+    hipStream_t side[kMaxSets] = {};  // streams 1.. of the overlapped schedule
+    std::vector<hipEvent_t> ev;  // cross-stream ordering events (timing disabled)
     void release();
 };
 
 // Optional device timing (om_set_timing): HIP event pairs on the launch stream.  Mode 1
-// brackets every launch (tagged with its OM_KT_* class); mode 2 brackets the whole
-// bounce-kernel family of a batch once (OM_KT_BOUNCE_SPAN, with its launch count), which
-// costs two events per batch instead of two per launch.
+// brackets every launch (tagged with its OM_KT_* class) and the call; mode 2 brackets only
+// the call (OM_KT_BOUNCE_SPAN, with its bounce-family launch count): two events per call.
 struct Timer {
     int mode = 0;
     std::vector<hipEvent_t> ev;   // pool, pairs (2i, 2i+1)
-    std::vector<int> cls;         // class of pair i since the last read
+    std::vector<int> cls;         // class of pair i since the last read (-1: open)
     std::vector<uint32_t> nl;     // launches inside pair i
     bool on() const { return mode != 0; }
-    void begin(hipStream_t st) {
-        if (!on()) return;
-        const size_t i = 2 * cls.size();
-        while (ev.size() < i + 2) {
+    // Opens pair i (recorded on `st`) and returns i; pairs may nest (a call around its launches).
+    int begin(hipStream_t st) {
+        if (!on()) return -1;
+        const size_t i = cls.size();
+        while (ev.size() < 2 * i + 2) {
             hipEvent_t e = nullptr;
-            if (hipEventCreate(&e) != hipSuccess) { mode = 0; return; }
+            if (hipEventCreate(&e) != hipSuccess) { mode = 0; return -1; }
             ev.push_back(e);
         }
-        (void)hipEventRecord(ev[i], st);
+        (void)hipEventRecord(ev[2 * i], st);
+        cls.push_back(-1);
+        nl.push_back(0);
+        return (int)i;
     }
-    void end(int c, hipStream_t st, uint32_t launches = 1) {
-        if (!on()) return;
-        (void)hipEventRecord(ev[2 * cls.size() + 1], st);
-        cls.push_back(c);
-        nl.push_back(launches);
+    void end(int i, int c, hipStream_t st, uint32_t launches = 1) {
+        if (!on() || i < 0) return;
+        (void)hipEventRecord(ev[2 * i + 1], st);
+        cls[i] = c;
+        nl[i] = launches;
     }
     void clear() { cls.clear(); nl.clear(); }
     void release() { for (auto e : ev) (void)hipEventDestroy(e); ev.clear(); clear(); }
@@ -66,6 +83,7 @@ struct Launch {
     bool count;
     int trace_mode;              // closest-hit kernel variant (om_render.hip MODE_*)
     uint32_t tail_bounce;        // first bounce run by the persistent tail kernel (0 = default)
+    uint32_t streams;            // fixed-spp calls: batches in flight (queue sets, streams), 1 = serial, <= kMaxSets
     Timer* timer;                // per-launch event timing (may be off)
     const uint32_t* tile_off;    // primary-ray candidate lists per 8x8 tile (null = traverse the BVH)
     const uint16_t* tile_idx;

@@ -32,7 +32,7 @@ using namespace omd;
 
 namespace omw {
 
-void Buffers::release() {
+void QueueSet::release() {
     for (int a = 0; a < 2; ++a) {
         for (int b = 0; b < 3; ++b) { if (q[a][b]) (void)hipFree(q[a][b]); q[a][b] = nullptr; }
         if (qr[a]) (void)hipFree(qr[a]); qr[a] = nullptr;
@@ -40,7 +40,17 @@ void Buffers::release() {
     if (res) (void)hipFree(res);
     if (res_id) (void)hipFree(res_id);
     if (counts) (void)hipFree(counts);
-    res = nullptr; res_id = nullptr; counts = nullptr; cap = 0; counts_n = 0;
+    res = nullptr; res_id = nullptr; counts = nullptr;
+}
+
+void Buffers::release() {
+    for (auto& s : set) s.release();
+    if (n0) (void)hipFree(n0);
+    n0 = nullptr; n0_cap = 0;
+    for (auto& st : side) { if (st) (void)hipStreamDestroy(st); st = nullptr; }
+    for (auto e : ev) (void)hipEventDestroy(e);
+    ev.clear();
+    cap = 0; counts_n = 0; nsets = 0;
 }
 
 namespace {
@@ -128,6 +138,8 @@ struct Gen {
     const om_pixel_stats* stats;
     const uint32_t* pixels;      // tile-ordered pixel list
     uint32_t n_pixels, by_pixel, batch;
+    const uint32_t* n0;          // fixed-spp calls: Stats.n per listed pixel at the call's start
+    uint32_t done;               // samples of the call before this batch (with n0)
     const uint32_t* tile_off;    // primary-ray candidate lists (null: traverse)
     const uint16_t* tile_idx;
 };
@@ -284,9 +296,19 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
                 const uint32_t s_local = (uint32_t)(i / R.n_pixels), k = (uint32_t)(i - (uint64_t)s_local * R.n_pixels);
                 const uint32_t pixel = R.pixels[k];
                 p_pixel = pixel;
-                const om_pixel_stats& ps = R.stats[R.by_pixel ? pixel : k];
-                const uint32_t s = ps.n + s_local;
-                live = s < P.spp_total && !(P.adaptive && (ps.flags & 1u));
+                // the sample index is the pixel's Stats.n (jitters[pixel.stats.n], render_thread.rs:188).
+                // Fixed-spp calls take it from the call-start snapshot plus the samples of earlier
+                // batches, so a batch never waits for the previous batch's accumulate; adaptive
+                // calls (one sample per batch) read the live Stats for n and the done flag.
+                uint32_t s;
+                if (R.n0) {
+                    s = R.n0[k] + R.done + s_local;
+                    live = s < P.spp_total;
+                } else {
+                    const om_pixel_stats& ps = R.stats[R.by_pixel ? pixel : k];
+                    s = ps.n + s_local;
+                    live = s < P.spp_total && !(P.adaptive && (ps.flags & 1u));
+                }
                 if (live) {
                     p.g = path_rng(P.skey, pixel, s);
                     const uint32_t line = pixel / P.width;
@@ -437,84 +459,120 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
     }
 }
 
-hipError_t grow(Buffers& B, uint64_t cap, uint32_t counts_n) {
-    if (cap > B.cap) {
-        uint32_t* cnt = B.counts;
-        const uint32_t cn = B.counts_n;
-        B.counts = nullptr;
-        B.release();
-        B.counts = cnt; B.counts_n = cn;
-        hipError_t e;
-        for (int a = 0; a < 2; ++a) {
-            for (int b = 0; b < 3; ++b) if ((e = hipMalloc(&B.q[a][b], cap * sizeof(float4))) != hipSuccess) return e;
-            if ((e = hipMalloc(&B.qr[a], cap * sizeof(uint4))) != hipSuccess) return e;
+// k_snapshot: n0[k] = Stats.n of listed pixel k at the start of a fixed-spp call.
+__global__ __launch_bounds__(256) void k_snapshot(const om_pixel_stats* __restrict__ stats, const uint32_t* __restrict__ pixels,
+                                                  uint32_t n_pixels, uint32_t by_pixel, uint32_t* __restrict__ n0) {
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    if (k < n_pixels) n0[k] = stats[by_pixel ? pixels[k] : k].n;
+}
+
+hipError_t grow(Buffers& B, uint64_t cap, uint32_t counts_n, int nsets) {
+    hipError_t e;
+    if (cap > B.cap || nsets > B.nsets) {
+        for (auto& s : B.set) s.release();
+        B.cap = 0; B.nsets = 0; B.counts_n = 0;
+        for (int k = 0; k < nsets; ++k) {
+            QueueSet& S = B.set[k];
+            for (int a = 0; a < 2; ++a) {
+                for (int b = 0; b < 3; ++b) if ((e = hipMalloc(&S.q[a][b], cap * sizeof(float4))) != hipSuccess) return e;
+                if ((e = hipMalloc(&S.qr[a], cap * sizeof(uint4))) != hipSuccess) return e;
+            }
+            if ((e = hipMalloc(&S.res, cap * sizeof(float4))) != hipSuccess) return e;
+            if ((e = hipMalloc(&S.res_id, cap * sizeof(uint32_t))) != hipSuccess) return e;
         }
-        if ((e = hipMalloc(&B.res, cap * sizeof(float4))) != hipSuccess) return e;
-        if ((e = hipMalloc(&B.res_id, cap * sizeof(uint32_t))) != hipSuccess) return e;
-        B.cap = cap;
+        B.cap = cap; B.nsets = nsets;
     }
     if (counts_n > B.counts_n) {
-        if (B.counts) (void)hipFree(B.counts);
-        B.counts = nullptr;
-        hipError_t e = hipMalloc(&B.counts, (size_t)counts_n * sizeof(uint32_t));
-        if (e != hipSuccess) return e;
+        for (int k = 0; k < B.nsets; ++k) {
+            QueueSet& S = B.set[k];
+            if (S.counts) (void)hipFree(S.counts);
+            S.counts = nullptr;
+            if ((e = hipMalloc(&S.counts, (size_t)counts_n * sizeof(uint32_t))) != hipSuccess) return e;
+        }
         B.counts_n = counts_n;
     }
     return hipSuccess;
 }
 
-Queue queue(Buffers& B, int k) { return Queue{B.q[k][0], B.q[k][1], B.q[k][2], B.qr[k]}; }
+Queue queue(QueueSet& B, int k) { return Queue{B.q[k][0], B.q[k][1], B.q[k][2], B.qr[k]}; }
 
-// One batch: bounce 0 .. tail_at-1 as per-bounce launches, then the tail launch.
+// One batch: bounce 0 .. tail_at-1 as per-bounce launches, then the tail launch; returns
+// the number of bounce-family launches.
 template <int TR, bool COUNT, bool MARCH>
-void run_batch(Buffers& B, const Launch& L, hipStream_t st, Seg G, const Gen& R, uint32_t depth_cap,
-               uint32_t tail_at, uint32_t lds) {
+uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Gen& R, uint32_t depth_cap,
+                   uint32_t tail_at, uint32_t lds) {
     Timer& tm = *L.timer;
-    const bool span = tm.mode == 2, each = tm.mode == 1;
-    if (span) tm.begin(st);
+    const bool each = tm.mode == 1;
     uint32_t launches = 0;
     for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
         const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
         const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
         if (bounce > 0 && bounce >= tail_at) {
             const uint32_t grid = (G.nseg + kTailSpb - 1u) / kTailSpb;
-            if (each) tm.begin(st);
+            const int ti = each ? tm.begin(st) : -1;
             hipLaunchKernelGGL((k_tail<TR, COUNT, MARCH>), dim3(grid), dim3(kBlk), lds, st, L.S, L.P, G, in, cin,
                                B.res, B.res_id, L.counters);
-            if (each) tm.end(OM_KT_TAIL, st);
-            if (span) tm.end(OM_KT_BOUNCE_SPAN, st, launches + 1u);
-            return;
+            tm.end(ti, OM_KT_TAIL, st);
+            return launches + 1u;
         }
         uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
-        if (each) tm.begin(st);
+        const int ti = each ? tm.begin(st) : -1;
         if (bounce == 0)
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, true>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
                                cin, out, cout, B.res, B.res_id, L.counters);
         else
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
                                cin, out, cout, B.res, B.res_id, L.counters);
-        if (each) tm.end(bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE, st);
+        tm.end(ti, bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE, st);
         ++launches;
     }
-    if (span) tm.end(OM_KT_BOUNCE_SPAN, st, launches);
+    return launches;
 }
 
 template <int TR>
-void run_tr(bool count, bool march, Buffers& B, const Launch& L, hipStream_t st, Seg G, const Gen& R,
-            uint32_t depth_cap, uint32_t tail_at, uint32_t lds) {
-    if (count && march) run_batch<TR, true, true>(B, L, st, G, R, depth_cap, tail_at, lds);
-    else if (count) run_batch<TR, true, false>(B, L, st, G, R, depth_cap, tail_at, lds);
-    else if (march) run_batch<TR, false, true>(B, L, st, G, R, depth_cap, tail_at, lds);
-    else run_batch<TR, false, false>(B, L, st, G, R, depth_cap, tail_at, lds);
+uint32_t run_tr(bool count, bool march, QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Gen& R,
+                uint32_t depth_cap, uint32_t tail_at, uint32_t lds) {
+    if (count && march) return run_batch<TR, true, true>(B, L, st, G, R, depth_cap, tail_at, lds);
+    if (count) return run_batch<TR, true, false>(B, L, st, G, R, depth_cap, tail_at, lds);
+    if (march) return run_batch<TR, false, true>(B, L, st, G, R, depth_cap, tail_at, lds);
+    return run_batch<TR, false, false>(B, L, st, G, R, depth_cap, tail_at, lds);
+}
+
+hipError_t ensure_events(Buffers& B, size_t n) {
+    while (B.ev.size() < n) {
+        hipEvent_t e = nullptr;
+        const hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (r != hipSuccess) return r;
+        B.ev.push_back(e);
+    }
+    return hipSuccess;
 }
 
 }  // namespace
 
+// Schedules:
+//   serial      (adaptive calls, or L.streams == 1) one batch after another on `st`; an
+//               adaptive batch's bounce 0 reads the Stats its predecessor's accumulate wrote.
+//   concurrent  (fixed spp, default) the call's samples split into batches of at most half
+//               the call, dealt round-robin to L.streams streams (`st` + side streams), each
+//               with its own queue set: two batches are in flight at once, so one batch's
+//               latency-bound phases (the drain of every launch, the late bounces, the tail)
+//               run beside the other's full ones.  Accumulates stay in sample order through
+//               events (acc i after acc i-1) and the call ends joined on `st`.  Sample indices
+//               come from the call-start Stats.n snapshot (n0), so every schedule renders
+//               identical bits.
+// Timing: mode 2 brackets the call once on `st` (OM_KT_BOUNCE_SPAN, with the call's
+// bounce-family launch count); mode 1 brackets every launch on its stream and the call.
 hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err) {
     const uint32_t n_px = L.n_pixels;
     if (n_px == 0 || L.P.sample_count == 0) return hipSuccess;
-    const uint64_t kMaxPaths = 1ull << 25;   // 33.5M paths per batch (~4.9 GB of queues)
-    const uint32_t batch = L.P.adaptive ? 1u : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));
+    const uint64_t kMaxPaths = 1ull << 25;   // 33.5M paths per batch (~4.9 GB of queues per set)
+    const uint32_t want = std::max<uint32_t>(1u, std::min<uint32_t>(L.streams, (uint32_t)kMaxSets));
+    const bool concurrent = !L.P.adaptive && want >= 2u && L.P.sample_count >= 2u;
+    uint32_t batch = L.P.adaptive ? 1u : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));
+    if (concurrent) batch = std::min<uint32_t>(batch, (L.P.sample_count + want - 1u) / want);
+    const uint32_t nb = (L.P.sample_count + batch - 1u) / batch;
+    const uint32_t ns = concurrent ? std::min<uint32_t>(want, nb) : 1u;
     const uint32_t depth_cap = L.P.max_depth > 1u ? L.P.max_depth : 1u;
     const uint32_t tail_at = L.tail_bounce ? L.tail_bounce : kTailDefault;
     int dev = 0;
@@ -526,7 +584,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (4096u / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
     const uint32_t segcap = (uint32_t)((max_paths + nseg - 1) / nseg);
-    hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg);
+    hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg, (int)ns);
     if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
     int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
     if (tr == TR_BVH4_LDS) tr = L.S.n_b4nodes == 0 ? TR_BVH2_LDS : (L.S.b4_lds_bytes ? TR_BVH4_LDS : TR_BVH4_GLOBAL);
@@ -540,35 +598,73 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     R.C = L.C; R.jitter = L.jitter; R.stats = L.stats; R.pixels = L.pixels; R.n_pixels = n_px;
     R.by_pixel = L.stats_by_pixel ? 1u : 0u;
     R.tile_off = L.tile_off; R.tile_idx = L.tile_idx;
-    for (uint32_t done = 0; done < L.P.sample_count;) {
+    R.n0 = nullptr; R.done = 0;
+    hipStream_t streams[kMaxSets] = {st, st, st, st};
+    Timer& tm = *L.timer;
+    const int call_ti = tm.begin(st);
+    if (!L.P.adaptive) {
+        if (n_px > B.n0_cap) {
+            if (B.n0) (void)hipFree(B.n0);
+            B.n0 = nullptr; B.n0_cap = 0;
+            if ((e = hipMalloc(&B.n0, (size_t)n_px * sizeof(uint32_t))) != hipSuccess) { err = "n0 allocation failed"; return e; }
+            B.n0_cap = n_px;
+        }
+        hipLaunchKernelGGL(k_snapshot, dim3((n_px + 255u) / 256u), dim3(256), 0, st, L.stats, L.pixels, n_px,
+                           R.by_pixel, B.n0);
+        R.n0 = B.n0;
+    }
+    // events: [0] call start on `st`, [k] side stream k joined, [kMaxSets + i] batch i accumulated
+    if (ns > 1) {
+        if ((e = ensure_events(B, kMaxSets + nb)) != hipSuccess) { err = "event creation failed"; return e; }
+        (void)hipEventRecord(B.ev[0], st);                       // side streams start after everything before the call
+        for (uint32_t k = 1; k < ns; ++k) {
+            if (!B.side[k] && (e = hipStreamCreateWithFlags(&B.side[k], hipStreamNonBlocking)) != hipSuccess) {
+                err = "side stream creation failed"; return e;
+            }
+            streams[k] = B.side[k];
+            (void)hipStreamWaitEvent(streams[k], B.ev[0], 0);
+        }
+    }
+    uint32_t launches = 0;
+    for (uint32_t i = 0, done = 0; i < nb; ++i) {
         const uint32_t b = std::min(batch, L.P.sample_count - done);
         const uint64_t paths = (uint64_t)n_px * b;
+        hipStream_t si = streams[i % ns];
+        QueueSet& QS = B.set[i % ns];
         Seg G;
         G.nseg = nseg;
         G.segcap = (uint32_t)((paths + nseg - 1) / nseg);
         R.batch = b;
+        R.done = done;
         switch (tr) {
-            case TR_BRUTE: run_tr<TR_BRUTE>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
-            case TR_CULLED: run_tr<TR_CULLED>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
-            case TR_BVH: run_tr<TR_BVH>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
-            case TR_SBVH_GLOBAL: run_tr<TR_SBVH_GLOBAL>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
-            case TR_BVH2_LDS: run_tr<TR_BVH2_LDS>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
-            case TR_BVH4_LDS: run_tr<TR_BVH4_LDS>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
-            case TR_BVH4_GLOBAL: run_tr<TR_BVH4_GLOBAL>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
-            default: run_tr<TR_BVH2_GLOBAL>(L.count, march, B, L, st, G, R, depth_cap, tail_at, lds); break;
+            case TR_BRUTE: launches += run_tr<TR_BRUTE>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
+            case TR_CULLED: launches += run_tr<TR_CULLED>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
+            case TR_BVH: launches += run_tr<TR_BVH>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
+            case TR_SBVH_GLOBAL: launches += run_tr<TR_SBVH_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
+            case TR_BVH2_LDS: launches += run_tr<TR_BVH2_LDS>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
+            case TR_BVH4_LDS: launches += run_tr<TR_BVH4_LDS>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
+            case TR_BVH4_GLOBAL: launches += run_tr<TR_BVH4_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
+            default: launches += run_tr<TR_BVH2_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
         }
+        if (ns > 1 && i > 0) (void)hipStreamWaitEvent(si, B.ev[kMaxSets + i - 1u], 0);   // Stats::add in sample order
         const uint32_t grid_a = (n_px + kBlk - 1) / kBlk;
-        if (L.timer->mode == 1) L.timer->begin(st);
+        const int ati = tm.mode == 1 ? tm.begin(si) : -1;
         if (L.count)
-            hipLaunchKernelGGL(k_accumulate<true>, dim3(grid_a), dim3(kBlk), 0, st, L.P, L.stats, L.pixels, n_px,
-                               L.stats_by_pixel ? 1u : 0u, b, B.res, B.res_id, L.S.bloom, L.counters);
+            hipLaunchKernelGGL(k_accumulate<true>, dim3(grid_a), dim3(kBlk), 0, si, L.P, L.stats, L.pixels, n_px,
+                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, L.counters);
         else
-            hipLaunchKernelGGL(k_accumulate<false>, dim3(grid_a), dim3(kBlk), 0, st, L.P, L.stats, L.pixels, n_px,
-                               L.stats_by_pixel ? 1u : 0u, b, B.res, B.res_id, L.S.bloom, L.counters);
-        if (L.timer->mode == 1) L.timer->end(OM_KT_ACCUMULATE, st);
+            hipLaunchKernelGGL(k_accumulate<false>, dim3(grid_a), dim3(kBlk), 0, si, L.P, L.stats, L.pixels, n_px,
+                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, L.counters);
+        tm.end(ati, OM_KT_ACCUMULATE, si);
+        if (ns > 1) (void)hipEventRecord(B.ev[kMaxSets + i], si);
         if ((e = hipGetLastError()) != hipSuccess) { err = "wavefront launch failed"; return e; }
         done += b;
     }
+    for (uint32_t k = 1; k < ns; ++k) {                           // the call ends joined on `st`
+        (void)hipEventRecord(B.ev[k], streams[k]);
+        (void)hipStreamWaitEvent(st, B.ev[k], 0);
+    }
+    tm.end(call_ti, OM_KT_BOUNCE_SPAN, st, launches);
     return hipSuccess;
 }
 
