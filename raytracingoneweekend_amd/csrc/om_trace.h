@@ -7,6 +7,21 @@
 
 namespace omd {
 
+// Slab-test min/max (kept as fminf/fmaxf: an inline-asm v_min/v_max variant that skips
+// LLVM's canonicalising v_max x,x of loop-carried operands measured 12% slower, because the
+// compiler drains every outstanding load before an asm statement).
+__device__ __forceinline__ float smin(float a, float b) { return fminf(a, b); }
+__device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
+__device__ __forceinline__ float smin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
+__device__ __forceinline__ float smax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+// near / far slab distances of one box: max(min(x), min(y), min(z), t_lo), min(max(x), max(y), max(z), t_hi)
+__device__ __forceinline__ float slab_near(float x0, float x1, float y0, float y1, float z0, float z1, float t_lo) {
+    return smax3(smin(x0, x1), smin(y0, y1), smax(smin(z0, z1), t_lo));
+}
+__device__ __forceinline__ float slab_far(float x0, float x1, float y0, float y1, float z0, float z1, float t_hi) {
+    return smin3(smax(x0, x1), smax(y0, y1), smin(smax(z0, z1), t_hi));
+}
+
 // Work counters (om_counters); compiled out (COUNT=false) of the production kernels so
 // they cost no registers — the bench counts work in a separate, identical launch.
 template <bool COUNT>
@@ -105,13 +120,13 @@ __device__ __forceinline__ int traced_bvh(const OmSceneDev& S, F3 o, F3 d, float
             float x0 = (L.lo[0] - o.x) * ix, x1 = (L.hi[0] - o.x) * ix;
             float y0 = (L.lo[1] - o.y) * iy, y1 = (L.hi[1] - o.y) * iy;
             float z0 = (L.lo[2] - o.z) * iz, z1 = (L.hi[2] - o.z) * iz;
-            const float ln = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-            const float lf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+            const float ln = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
+            const float lf = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
             x0 = (R.lo[0] - o.x) * ix; x1 = (R.hi[0] - o.x) * ix;
             y0 = (R.lo[1] - o.y) * iy; y1 = (R.hi[1] - o.y) * iy;
             z0 = (R.lo[2] - o.z) * iz; z1 = (R.hi[2] - o.z) * iz;
-            const float rn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-            const float rf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+            const float rn = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
+            const float rf = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
             const bool hl = ln <= lf, hr = rn <= rf;
             if (hl && hr) {
                 const bool left_first = ln <= rn;
@@ -140,8 +155,8 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
         const float x0 = __builtin_fmaf(A.lo[0], ix, nox), x1 = __builtin_fmaf(A.hi[0], ix, nox);
         const float y0 = __builtin_fmaf(A.lo[1], iy, noy), y1 = __builtin_fmaf(A.hi[1], iy, noy);
         const float z0 = __builtin_fmaf(A.lo[2], iz, noz), z1 = __builtin_fmaf(A.hi[2], iz, noz);
-        const float n0 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-        const float f0 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        const float n0 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
+        const float f0 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
         if (!(n0 > f0)) offer(S, A.gi, o, d, tmin, closest, best, w);
     }
 }
@@ -195,8 +210,8 @@ __device__ __forceinline__ int traced_sbvh(const OmSceneDev& S, const OmSkipNode
         const float x0 = __builtin_fmaf(N.lo[0], ix, nox), x1 = __builtin_fmaf(N.hi[0], ix, nox);
         const float y0 = __builtin_fmaf(N.lo[1], iy, noy), y1 = __builtin_fmaf(N.hi[1], iy, noy);
         const float z0 = __builtin_fmaf(N.lo[2], iz, noz), z1 = __builtin_fmaf(N.hi[2], iz, noz);
-        const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-        const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        const float tn = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
+        const float tf = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
         if (!(tn > tf)) {
             if (N.leaf == 0xFFFFFFFFu) { node++; continue; }
             const uint32_t first = N.leaf >> 8, cnt = N.leaf & 255u;
@@ -411,13 +426,13 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
         float x0 = __builtin_fmaf(N.lo0[0], ix, nox), x1 = __builtin_fmaf(N.hi0[0], ix, nox);
         float y0 = __builtin_fmaf(N.lo0[1], iy, noy), y1 = __builtin_fmaf(N.hi0[1], iy, noy);
         float z0 = __builtin_fmaf(N.lo0[2], iz, noz), z1 = __builtin_fmaf(N.hi0[2], iz, noz);
-        const float n0 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-        const float f0 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        const float n0 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
+        const float f0 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
         x0 = __builtin_fmaf(N.lo1[0], ix, nox); x1 = __builtin_fmaf(N.hi1[0], ix, nox);
         y0 = __builtin_fmaf(N.lo1[1], iy, noy); y1 = __builtin_fmaf(N.hi1[1], iy, noy);
         z0 = __builtin_fmaf(N.lo1[2], iz, noz); z1 = __builtin_fmaf(N.hi1[2], iz, noz);
-        const float n1 = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-        const float f1 = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+        const float n1 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
+        const float f1 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
         const bool h0 = !(n0 > f0), h1 = !(n1 > f1);
         if (h0 && h1) {                                 // near child next, far child pushed
             const bool swap = n1 < n0;
@@ -475,8 +490,8 @@ __device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node
             const float x0 = __builtin_fmaf(N.lox[k], ix, nox), x1 = __builtin_fmaf(N.hix[k], ix, nox);
             const float y0 = __builtin_fmaf(N.loy[k], iy, noy), y1 = __builtin_fmaf(N.hiy[k], iy, noy);
             const float z0 = __builtin_fmaf(N.loz[k], iz, noz), z1 = __builtin_fmaf(N.hiz[k], iz, noz);
-            const float tn = fmaxf(fmaxf(fminf(x0, x1), fminf(y0, y1)), fmaxf(fminf(z0, z1), t_lo));
-            const float tf = fminf(fminf(fmaxf(x0, x1), fmaxf(y0, y1)), fminf(fmaxf(z0, z1), t_hi));
+            const float tn = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
+            const float tf = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
             const uint32_t c = N.child[k];
             const bool h = !(tn > tf) && c != OM_EMPTY;
             key[k] = h ? tn : INFINITY;

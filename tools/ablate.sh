@@ -24,6 +24,7 @@ declare -A V=(
   [tspb1]="$COMMON $DEV -DOM_WF_TAIL_SPB=1"
   [tspb2]="$COMMON $DEV -DOM_WF_TAIL_SPB=2"
   [shade2x]="$COMMON $DEV -DOM_ABLATE_SHADE2X"
+  [b512w6]="$COMMON $DEV -DOM_WF_BLOCK=512 -DOM_WF_WAVES=6"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
@@ -36,7 +37,7 @@ if [ "$1" = resources ]; then
 fi
 if [ "$1" = build ]; then
   mkdir -p _abl
-  for k in "${!V[@]}"; do
+  for k in ${VARIANTS:-${!V[@]}}; do
     ( /opt/rocm/bin/hipcc ${V[$k]} -shared -o _abl/lib_$k.so $SRC/om_world.cpp $SRC/om_bvh.cpp $SRC/om_image.cpp $SRC/om_tiles.cpp -x hip $SRC/om_render.hip $SRC/om_wavefront.hip $SRC/om_display.hip \
       > _abl/$k.log 2>&1 && echo "built $k" ) &
   done
