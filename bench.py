@@ -51,6 +51,7 @@ def make_scene(name, om_or_oracle):
         return om_or_oracle.marched_scene()
     return om_or_oracle.random_scene(SCENE_SEED, grid_half=50, extras=False)
 PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md; FMA = 2 flop)
+ISSUE_PEAK_TFLOPS = 78.6  # one f32 op per lane per cycle: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz (no FMA)
 PEAK_HBM_GBS = 8000.0
 
 # Algorithmic FP32 work per counted unit, counted from om_device.h /
@@ -259,6 +260,7 @@ def main():
             traffic, traffic_src = pm["hbm_bytes_per_launch"], pm["source"]
         roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": traffic,
+                "issue_peak": ISSUE_PEAK_TFLOPS, "frac_of_issue_peak": round(achieved_tflops / ISSUE_PEAK_TFLOPS, 4),
                 "kernel": "render_kernel (megakernel)" if mega else "k_bounce0+k_bounce+k_tail (fused trace+shade)",
                 "launches_per_step": round(launches / args.steps, 2),
                 "avg_launch_ms": round(per_launch_s * 1e3, 4),

@@ -206,8 +206,8 @@ om_status om_set_counting(om_ctx* ctx, int32_t enable);
  *                          persistent tail launch, then accumulate
  *   OM_PIPELINE_MEGAKERNEL one persistent-path kernel per call
  *   OM_PIPELINE_AUTO       (default) the faster one measured for the call: megakernel for
- *                          worlds with marched primitives and for adaptive renders, else
- *                          wavefront */
+ *                          adaptive renders and for worlds with marched primitives when
+ *                          om_set_streams is 1, else wavefront */
 enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1, OM_PIPELINE_AUTO = 2 };
 om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
 /* Wavefront pipeline: bounces >= `bounce` are finished by one persistent tail launch

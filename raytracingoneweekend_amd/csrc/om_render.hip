@@ -442,12 +442,14 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     }
     if (threads == 0) return OM_OK;
     int pipeline = c->pipeline;
-    // AUTO: the measured faster pipeline: the megakernel for marched SDFs (C2:
-    // 916 vs 790 Msamples/s) and for adaptive sampling (one sample per pixel per wavefront
-    // pass; C1 adaptive: 2804 vs 553 credited Msamples/s), else the wavefront.
-    if (pipeline == OM_PIPELINE_AUTO)
-        pipeline = ((c->scene.n_msph + c->scene.n_mbox + c->scene.n_mtor) || p->adaptive) ? OM_PIPELINE_MEGAKERNEL
-                                                                                          : OM_PIPELINE_WAVEFRONT;
+    // AUTO: the measured faster pipeline: the megakernel for adaptive sampling
+    // (one sample per pixel per wavefront pass; C1 adaptive: 2804 vs 553 credited Msamples/s)
+    // and for marched SDFs when batches run serially (C2: 916 vs 790); else the wavefront
+    // (C2 with concurrent batches: 1111 vs 976, C1: 5722 vs 3142).
+    if (pipeline == OM_PIPELINE_AUTO) {
+        const bool marched = (c->scene.n_msph + c->scene.n_mbox + c->scene.n_mtor) != 0;
+        pipeline = (p->adaptive || (marched && c->wf_streams < 2)) ? OM_PIPELINE_MEGAKERNEL : OM_PIPELINE_WAVEFRONT;
+    }
     int mode = c->kernel;
     if (mode == OM_KERNEL_AUTO) mode = OM_KERNEL_BVH2;
     if (pipeline == OM_PIPELINE_WAVEFRONT) {

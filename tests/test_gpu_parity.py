@@ -193,16 +193,21 @@ def test_tail_bounce_is_bit_identical(om, oracle, tail):
 
 
 def test_auto_pipeline_choice(om, oracle):
-    """OM_PIPELINE_AUTO: megakernel for worlds with marched SDFs, wavefront otherwise (the
-    faster one on C2 / C1), observed through the per-launch timing classes; bit-exact."""
+    """OM_PIPELINE_AUTO: the megakernel for adaptive renders and for marched SDFs with serial
+    batches, the wavefront otherwise (the faster one measured on C1 / C2),
+    observed through the per-launch timing classes; bit-exact."""
     import ctypes as C
     from raytracingoneweekend_amd import _lib as L
     W, H = 24, 16
-    for world, oworld, adaptive, want in ((om.marched_scene(), oracle.marched_scene(), False, "megakernel"),
-                                          (om.random_scene(0x5EED), oracle.random_scene(0x5EED), True, "megakernel"),
-                                          (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, "bounce0")):
+    for world, oworld, adaptive, streams, want in (
+            (om.marched_scene(), oracle.marched_scene(), False, 1, "megakernel"),
+            (om.marched_scene(), oracle.marched_scene(), False, 2, "bounce0"),
+            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), True, 2, "megakernel"),
+            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, 1, "bounce0"),
+            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, 2, "bounce0")):
         cam = om.default_camera(W / H)
         fz = world.freeze(cam)                                    # pipeline="auto" is the default
+        L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
         L.check(L.lib.om_set_timing(fz.ctx, 1), fz.ctx)
         pix = om.PixelsBox.new(W * H)
         om.render(cam, fz, 50, 0.001, 100.0, 8, W, H, pix, seed=8, march_steps=256, adaptive=adaptive)
