@@ -87,6 +87,24 @@ __host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
 #endif
 constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
+// Work distribution inside a bounce workgroup.  1 (default): every wave takes 64-path
+// chunks of the segment from an LDS counter and appends its survivors with one LDS atomic,
+// so the 8 waves never wait for each other; 0: the block walks the segment in 512-path
+// steps with a block-wide ballot scan (two barriers per step, every wave waits for the
+// slowest).  Both produce identical bits: a path's results are keyed by its slot and its
+// RNG by (pixel, sample), never by its queue position.
+#ifndef OM_WF_WAVEQ
+#define OM_WF_WAVEQ 1
+#endif
+// Segment capacity rounded up to whole waves (0: exact split), so that a bounce-0 wave is
+// exactly one 8x8 tile of one sample (tile-ordered pixel lists hold whole tiles).
+#ifndef OM_WF_ALIGN
+#define OM_WF_ALIGN 64
+#endif
+__host__ __device__ inline uint32_t seg_capacity(uint64_t paths, uint32_t nseg) {
+    const uint64_t c = (paths + nseg - 1) / nseg;
+    return OM_WF_ALIGN > 1 ? (uint32_t)((c + OM_WF_ALIGN - 1) / OM_WF_ALIGN * OM_WF_ALIGN) : (uint32_t)c;
+}
 
 extern __shared__ __attribute__((aligned(16))) uint4 wf_lds[];
 
@@ -280,12 +298,23 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
         if (threadIdx.x == 0) count_out[blockIdx.x] = 0u;
         return;
     }
+#if OM_WF_WAVEQ
+    __shared__ uint32_t q_next, q_out;
+    if (threadIdx.x == 0) { q_next = kBlk / 64u; q_out = 0u; }
+    __syncthreads();
+#endif
     const Tracer T = stage_scene<TR>(S);
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
     WorkT<COUNT> w;
     uint32_t segs = 0, run = 0;
+#if OM_WF_WAVEQ
+    const uint32_t lane = __lane_id();
+    for (uint32_t chunk = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); chunk * 64u < n;) {   // wave-uniform
+        const uint32_t jj = chunk * 64u + lane;
+#else
     for (uint32_t base = 0; base < n; base += kBlk) {
         const uint32_t jj = base + threadIdx.x;
+#endif
         bool keep = false;
         Path p;
         uint32_t p_pixel = 0;
@@ -357,11 +386,26 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
                 if (COUNT) segs++;
             }
         }
+#if OM_WF_WAVEQ
+        const uint64_t m = __ballot(keep);
+        uint32_t obase = 0u, nc = 0u;
+        if (lane == 0) {
+            obase = m ? atomicAdd(&q_out, (uint32_t)__popcll(m)) : 0u;
+            nc = atomicAdd(&q_next, 1u);
+        }
+        obase = __builtin_amdgcn_readfirstlane(obase);
+        chunk = __builtin_amdgcn_readfirstlane(nc);
+        if (keep) store_path(out, seg0 + obase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), p);
+    }
+    __syncthreads();
+    run = q_out;
+#else
         uint32_t tot;
         const uint32_t j = block_scan(keep, tot);
         if (keep) store_path(out, seg0 + run + j, p);
         run += tot;
     }
+#endif
     if (threadIdx.x == 0) count_out[blockIdx.x] = run;
     if (COUNT) {
         flush_counter(counters, OMC_SEGMENTS, segs);
@@ -583,7 +627,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     // segments: ~4096 lanes per CU (16 workgroups of 256), a multiple of the tail grouping
     uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (4096u / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
-    const uint32_t segcap = (uint32_t)((max_paths + nseg - 1) / nseg);
+    const uint32_t segcap = seg_capacity(max_paths, nseg);
     hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg, (int)ns);
     if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
     int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
@@ -633,7 +677,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
         QueueSet& QS = B.set[i % ns];
         Seg G;
         G.nseg = nseg;
-        G.segcap = (uint32_t)((paths + nseg - 1) / nseg);
+        G.segcap = seg_capacity(paths, nseg);
         R.batch = b;
         R.done = done;
         switch (tr) {

@@ -25,6 +25,11 @@ declare -A V=(
   [tspb2]="$COMMON $DEV -DOM_WF_TAIL_SPB=2"
   [shade2x]="$COMMON $DEV -DOM_ABLATE_SHADE2X"
   [b512w6]="$COMMON $DEV -DOM_WF_BLOCK=512 -DOM_WF_WAVES=6"
+  # bounce work distribution (bit-identical): block-step scan instead of per-wave LDS queues,
+  # unaligned segments, both (the r01_v6 kernel)
+  [waveq0]="$COMMON $DEV -DOM_WF_WAVEQ=0"
+  [align1]="$COMMON $DEV -DOM_WF_ALIGN=1"
+  [v6]="$COMMON $DEV -DOM_WF_WAVEQ=0 -DOM_WF_ALIGN=1"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
