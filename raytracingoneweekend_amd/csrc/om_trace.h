@@ -22,6 +22,20 @@ __device__ __forceinline__ float slab_far(float x0, float x1, float y0, float y1
     return smin3(smax(x0, x1), smax(y0, y1), smin(smax(z0, z1), t_hi));
 }
 
+// Inverse direction component for the conservative slab tests only (never an output value):
+// the hardware reciprocal (1 ulp) instead of the correctly rounded division, ~10 VALU each.
+// Boxes are inflated by 1e-3*(1+extent) and the t window is loosened by 1e-4 relative, far
+// beyond its error; the component is kept >= 1e-20 in magnitude, so the result is finite.
+// OM_EXACT_INVDIR restores the division (timing ablation).
+__device__ __forceinline__ float inv_dir(float c) {
+    const float k = fabsf(c) > 1e-20f ? c : copysignf(1e-20f, c);
+#ifdef OM_EXACT_INVDIR
+    return 1.0f / k;
+#else
+    return __builtin_amdgcn_rcpf(k);
+#endif
+}
+
 // Work counters (om_counters); compiled out (COUNT=false) of the production kernels so
 // they cost no registers — the bench counts work in a separate, identical launch.
 template <bool COUNT>
@@ -195,9 +209,9 @@ __device__ __forceinline__ int traced_sbvh(const OmSceneDev& S, const OmSkipNode
                                            F3 o, F3 d, float tmin, float& closest, Wk& w) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return traced_brute<false, Wk>(S, o, d, tmin, closest, w);
     int best = -1;
-    const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
-    const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
-    const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    const float ix = inv_dir(d.x);
+    const float iy = inv_dir(d.y);
+    const float iz = inv_dir(d.z);
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
@@ -387,9 +401,9 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
                                             F3 o, F3 d, float tmin, float& closest, Wk& w) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
-    const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
-    const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
-    const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    const float ix = inv_dir(d.x);
+    const float iy = inv_dir(d.y);
+    const float iz = inv_dir(d.z);
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, tmin * 0.5f - 1e-3f, closest, best, w);
     const uint32_t e = toff[tile + 1];
@@ -403,9 +417,9 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
                                            F3 o, F3 d, float tmin, float& closest, Wk& w) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
-    const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
-    const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
-    const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    const float ix = inv_dir(d.x);
+    const float iy = inv_dir(d.y);
+    const float iz = inv_dir(d.z);
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
@@ -463,9 +477,9 @@ __device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node
                                            F3 o, F3 d, float tmin, float& closest, Wk& w) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
-    const float ix = 1.0f / (fabsf(d.x) > 1e-20f ? d.x : copysignf(1e-20f, d.x));
-    const float iy = 1.0f / (fabsf(d.y) > 1e-20f ? d.y : copysignf(1e-20f, d.y));
-    const float iz = 1.0f / (fabsf(d.z) > 1e-20f ? d.z : copysignf(1e-20f, d.z));
+    const float ix = inv_dir(d.x);
+    const float iy = inv_dir(d.y);
+    const float iz = inv_dir(d.z);
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);

@@ -98,6 +98,10 @@ constexpr uint32_t kTailDefault = 16;                             // first bounc
 #endif
 // Segment capacity rounded up to whole waves (0: exact split), so that a bounce-0 wave is
 // exactly one 8x8 tile of one sample (tile-ordered pixel lists hold whole tiles).
+// Queue segments (= bounce workgroups) per CU: OM_WF_LANES_PER_CU / OM_WF_BLOCK.
+#ifndef OM_WF_LANES_PER_CU
+#define OM_WF_LANES_PER_CU 4096
+#endif
 #ifndef OM_WF_ALIGN
 #define OM_WF_ALIGN 64
 #endif
@@ -625,7 +629,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint64_t max_paths = (uint64_t)n_px * batch;
     // segments: ~4096 lanes per CU (16 workgroups of 256), a multiple of the tail grouping
-    uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (4096u / kBlk));
+    uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (OM_WF_LANES_PER_CU / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
     const uint32_t segcap = seg_capacity(max_paths, nseg);
     hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg, (int)ns);

@@ -30,6 +30,13 @@ declare -A V=(
   [waveq0]="$COMMON $DEV -DOM_WF_WAVEQ=0"
   [align1]="$COMMON $DEV -DOM_WF_ALIGN=1"
   [v6]="$COMMON $DEV -DOM_WF_WAVEQ=0 -DOM_WF_ALIGN=1"
+  # segments per CU (lanes per CU / workgroup size)
+  [b1024l8]="$COMMON $DEV -DOM_WF_BLOCK=1024 -DOM_WF_WAVES=8 -DOM_WF_LANES_PER_CU=8192"
+  # correctly rounded 1/d for the slab tests (the default uses the hardware reciprocal)
+  [invdiv]="$COMMON $DEV -DOM_EXACT_INVDIR"
+  [lpc2k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=2048"
+  [lpc8k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=8192"
+  [lpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=16384"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
