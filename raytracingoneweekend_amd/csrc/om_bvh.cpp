@@ -255,32 +255,39 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     } e{b, fw, fw.snodes, fw.srecs, leaf_first};
     e.rec(root);
 
-    // compressed BVH2: both child boxes in the parent (one 64-B read per visit)
+    // compressed BVH2: both child boxes in the parent (one 64-B read per visit), emitted
+    // breadth-first so the top levels, which every ray visits, are the first nodes: a tree
+    // too big for LDS stages that prefix there (om_wavefront.hip, OM_WF_HYB_BYTES).
     struct Emit2 {
         const Builder& b; const std::vector<uint32_t>& leaf_first; std::vector<OmBvh2Node>& out;
         std::vector<uint32_t>& leaves;
+        std::vector<std::pair<uint32_t, uint32_t>> q;   // (builder node, output index)
         uint32_t code(uint32_t c) {
             const OmBvhNode& n = b.nodes[c];
             if (n.left < 0) {
                 leaves.push_back((leaf_first[c] << 8) | (uint32_t)n.right);
                 return OM_LEAF | (uint32_t)(leaves.size() - 1);
             }
-            return rec(c);
-        }
-        uint32_t rec(uint32_t n) {
-            const uint32_t idx = (uint32_t)out.size();
             out.push_back(OmBvh2Node{});
-            const OmBvhNode& src = b.nodes[n];
-            const OmBvhNode& L = b.nodes[(uint32_t)src.left];
-            const OmBvhNode& R = b.nodes[(uint32_t)src.right];
-            OmBvh2Node o{};
-            for (int i = 0; i < 3; ++i) { o.lo0[i] = L.lo[i]; o.hi0[i] = L.hi[i]; o.lo1[i] = R.lo[i]; o.hi1[i] = R.hi[i]; }
-            o.c0 = code((uint32_t)src.left);
-            o.c1 = code((uint32_t)src.right);
-            out[idx] = o;
-            return idx;
+            q.emplace_back(c, (uint32_t)(out.size() - 1));
+            return (uint32_t)(out.size() - 1);
         }
-    } e2{b, leaf_first, fw.b2nodes, fw.b2leaves};
+        void rec(uint32_t root) {
+            out.push_back(OmBvh2Node{});
+            q.emplace_back(root, 0u);
+            for (size_t h = 0; h < q.size(); ++h) {
+                const uint32_t n = q[h].first, idx = q[h].second;
+                const OmBvhNode& src = b.nodes[n];
+                const OmBvhNode& L = b.nodes[(uint32_t)src.left];
+                const OmBvhNode& R = b.nodes[(uint32_t)src.right];
+                OmBvh2Node o{};
+                for (int i = 0; i < 3; ++i) { o.lo0[i] = L.lo[i]; o.hi0[i] = L.hi[i]; o.lo1[i] = R.lo[i]; o.hi1[i] = R.hi[i]; }
+                o.c0 = code((uint32_t)src.left);
+                o.c1 = code((uint32_t)src.right);
+                out[idx] = o;
+            }
+        }
+    } e2{b, leaf_first, fw.b2nodes, fw.b2leaves, {}};
     fw.b2nodes.clear();
     fw.b2leaves.clear();
     if (b.nodes[root].left < 0) {            // a single leaf: one node, second child an empty leaf
@@ -300,7 +307,7 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     // depth of the compressed tree (the traversal's stack bound)
     std::vector<uint32_t> depth(fw.b2nodes.size(), 1);
     fw.b2_depth = 1;
-    for (uint32_t i = 0; i < fw.b2nodes.size(); ++i) {   // parents precede children (DFS)
+    for (uint32_t i = 0; i < fw.b2nodes.size(); ++i) {   // parents precede children (BFS)
         for (uint32_t c : {fw.b2nodes[i].c0, fw.b2nodes[i].c1})
             if (!(c & OM_LEAF)) { depth[c] = depth[i] + 1; fw.b2_depth = std::max(fw.b2_depth, depth[c]); }
     }

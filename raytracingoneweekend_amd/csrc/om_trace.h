@@ -411,10 +411,13 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
     return best;
 }
 
-template <int DEPTH, int STRIDE, class Wk>
+// HYB: only nodes [0, nl) are in `nodes` (the breadth-first prefix staged in LDS); the
+// others are read from `gnodes` (global memory, through L2).
+template <int DEPTH, int STRIDE, class Wk, bool HYB = false>
 __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node* nodes, const uint32_t* leaves,
                                            const OmAffineTest* recs, uint16_t* stk,
-                                           F3 o, F3 d, float tmin, float& closest, Wk& w) {
+                                           F3 o, F3 d, float tmin, float& closest, Wk& w,
+                                           const OmBvh2Node* gnodes = nullptr, uint32_t nl = 0) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
     const float ix = inv_dir(d.x);
@@ -434,7 +437,7 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
             cur = stk[sp * STRIDE];
             continue;
         }
-        const OmBvh2Node N = nodes[cur];
+        const OmBvh2Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
         w.add_pre(2);
         const float t_hi = closest * 1.0001f + 1e-3f;
         float x0 = __builtin_fmaf(N.lo0[0], ix, nox), x1 = __builtin_fmaf(N.hi0[0], ix, nox);

@@ -98,6 +98,14 @@ constexpr uint32_t kTailDefault = 16;                             // first bounc
 #endif
 // Segment capacity rounded up to whole waves (0: exact split), so that a bounce-0 wave is
 // exactly one 8x8 tile of one sample (tile-ordered pixel lists hold whole tiles).
+// A BVH2 too big for LDS (S-10k: 213 KB) stages its breadth-first prefix, up to this many
+// bytes of nodes, into LDS; deeper nodes are read through L2 (0 = every node from L2).
+#ifndef OM_WF_HYB_BYTES
+#define OM_WF_HYB_BYTES 24576
+#endif
+__host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
+    return S.b2_lds_bytes ? 0u : (S.n_b2nodes < OM_WF_HYB_BYTES / 64u ? S.n_b2nodes : OM_WF_HYB_BYTES / 64u);
+}
 // Queue segments (= bounce workgroups) per CU: OM_WF_LANES_PER_CU / OM_WF_BLOCK.
 #ifndef OM_WF_LANES_PER_CU
 #define OM_WF_LANES_PER_CU 4096
@@ -196,6 +204,8 @@ __device__ __forceinline__ void store_path(const Queue& Q, uint64_t i, const Pat
 // the per-lane stack ([stack][nodes][leaf table]), or read through L2.
 struct Tracer {
     const OmBvh2Node* b2n;
+    uint32_t nl;             // TR_BVH2_GLOBAL: nodes [0, nl) staged in LDS at b2l
+    const OmBvh2Node* b2l;
     const OmBvh4Node* b4n;
     const uint32_t* bl;
     const OmAffineTest* recs;
@@ -207,6 +217,15 @@ __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every 
     Tracer t;
     t.stk = (uint16_t*)wf_lds + threadIdx.x;
     t.b2n = S.b2nodes; t.b4n = S.b4nodes; t.bl = S.b2leaves; t.recs = S.srecs;
+    t.nl = 0; t.b2l = S.b2nodes;
+    if (TR == TR_BVH2_GLOBAL && hyb_nodes(S)) {
+        t.nl = hyb_nodes(S);
+        uint4* dst = wf_lds + stack_bytes<TR>(S) / 16u;
+        const uint4* sn = (const uint4*)S.b2nodes;
+        for (uint32_t i = threadIdx.x; i < t.nl * 4u; i += kBlk) dst[i] = sn[i];
+        __syncthreads();
+        t.b2l = (const OmBvh2Node*)dst;
+    }
     if (TR == TR_BVH2_LDS || TR == TR_BVH4_LDS) {
         const uint32_t nn = TR == TR_BVH2_LDS ? S.n_b2nodes * 4u : S.n_b4nodes * 7u;   // uint4 per node
         const uint4* sn = TR == TR_BVH2_LDS ? (const uint4*)S.b2nodes : (const uint4*)S.b4nodes;
@@ -229,7 +248,9 @@ __device__ __forceinline__ int trace(const OmSceneDev& S, const OmParamsDev& P, 
     closest = P.tmax;
     int best;
     if (TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) best = traced_bvh4<kBlk>(S, T.b4n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
-    else if (TR == TR_BVH2_LDS || TR == TR_BVH2_GLOBAL) best = traced_bvh2<kStackDepth, kBlk>(S, T.b2n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
+    else if (TR == TR_BVH2_LDS) best = traced_bvh2<kStackDepth, kBlk>(S, T.b2n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
+    else if (TR == TR_BVH2_GLOBAL)
+        best = traced_bvh2<kStackDepth, kBlk, Wk, true>(S, T.b2l, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w, T.b2n, T.nl);
     else if (TR == TR_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
     else if (TR == TR_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
     else best = traced_brute<TR == TR_CULLED>(S, o, d, P.tmin, closest, w);
@@ -638,7 +659,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     if (tr == TR_BVH4_LDS) tr = L.S.n_b4nodes == 0 ? TR_BVH2_LDS : (L.S.b4_lds_bytes ? TR_BVH4_LDS : TR_BVH4_GLOBAL);
     if (tr == TR_BVH2_LDS) tr = L.S.n_b2nodes == 0 ? TR_BVH : (L.S.b2_lds_bytes ? TR_BVH2_LDS : TR_BVH2_GLOBAL);
     const uint32_t lds = tr == TR_BVH2_LDS ? stack_bytes<TR_BVH2_LDS>(L.S) + L.S.b2_lds_bytes
-                       : tr == TR_BVH2_GLOBAL ? stack_bytes<TR_BVH2_GLOBAL>(L.S)
+                       : tr == TR_BVH2_GLOBAL ? stack_bytes<TR_BVH2_GLOBAL>(L.S) + hyb_nodes(L.S) * 64u
                        : tr == TR_BVH4_LDS ? stack_bytes<TR_BVH4_LDS>(L.S) + L.S.b4_lds_bytes
                        : tr == TR_BVH4_GLOBAL ? stack_bytes<TR_BVH4_GLOBAL>(L.S) : 0u;
     const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;

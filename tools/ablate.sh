@@ -34,6 +34,10 @@ declare -A V=(
   [b1024l8]="$COMMON $DEV -DOM_WF_BLOCK=1024 -DOM_WF_WAVES=8 -DOM_WF_LANES_PER_CU=8192"
   # correctly rounded 1/d for the slab tests (the default uses the hardware reciprocal)
   [invdiv]="$COMMON $DEV -DOM_EXACT_INVDIR"
+  # S-10k: bytes of breadth-first BVH2 prefix staged in LDS (0 = all nodes through L2)
+  [hyb0]="$COMMON $DEV -DOM_WF_HYB_BYTES=0"
+  [hyb16k]="$COMMON $DEV -DOM_WF_HYB_BYTES=16384"
+  [hyb40k]="$COMMON $DEV -DOM_WF_HYB_BYTES=40960"
   [lpc2k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=2048"
   [lpc8k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=8192"
   [lpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=16384"
