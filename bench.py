@@ -305,6 +305,7 @@ def main():
             "work": {"segments_per_sample": round(ctr.segments / max(1, ctr.samples), 4),
                      "prim_tests_per_segment": round(ctr.prim_tests / max(1, ctr.segments), 3),
                      "box_tests_per_segment": round(ctr.pre_tests / max(1, ctr.segments), 3),
+                     "march_steps_per_segment": round(ctr.march_steps / max(1, ctr.segments), 3),
                      "gsegments_per_s": round(ctr.segments * world_size / elapsed / 1e9, 4)},
             "cpu_baseline": cpu,
         }

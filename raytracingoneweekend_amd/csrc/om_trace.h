@@ -246,59 +246,157 @@ __device__ __forceinline__ int traced_sbvh(const OmSceneDev& S, const OmSkipNode
     return best;
 }
 
-// unstuck (hits.rs:336-365) + sphere-tracing loop (hits.rs:287-333).
-// Returns the marched winner's global index or -1; `t` receives the hit t.
-template <class Wk>
-__device__ __forceinline__ int march(const OmSceneDev& S, F3 o, F3 d, float tmin, float tmax, float closest,
-                                     uint32_t steps, float& t_hit, Wk& w) {
+// The marched objects of a world, seen by the march loop through one of two views:
+//  MarchedArrays  the scene arrays, any count (each step reloads every object's parameters
+//                 with scalar loads: runtime-bounded loops over memory);
+//  MarchedRegs    a copy of at most KS spheres, KB boxes and KT tori taken once before the
+//                 loop, so the parameters stay in (scalar) registers across the steps.
+// Both visit the objects in the same order with the same arithmetic.
+struct MarchedArrays {
+    static constexpr uint32_t KS = 0u, KB = 0u, KT = 0u;      // 0: unbounded
+    const OmMSphere* s; const OmMBox* b; const OmMTorus* t;
+    uint32_t ns, nb, nt;
+    __device__ explicit MarchedArrays(const OmSceneDev& S)
+        : s(S.msph), b(S.mbox), t(S.mtor), ns(S.n_msph), nb(S.n_mbox), nt(S.n_mtor) {}
+};
+template <uint32_t KS_, uint32_t KB_, uint32_t KT_>
+struct MarchedRegs {
+    static constexpr uint32_t KS = KS_, KB = KB_, KT = KT_;
+    OmMSphere s[KS]; OmMBox b[KB]; OmMTorus t[KT];
+    uint32_t ns, nb, nt;
+    __device__ explicit MarchedRegs(const OmSceneDev& S) : ns(S.n_msph), nb(S.n_mbox), nt(S.n_mtor) {
+#pragma unroll
+        for (uint32_t i = 0; i < KS; ++i) if (i < ns) s[i] = S.msph[i];
+#pragma unroll
+        for (uint32_t i = 0; i < KB; ++i) if (i < nb) b[i] = S.mbox[i];
+#pragma unroll
+        for (uint32_t i = 0; i < KT; ++i) if (i < nt) t[i] = S.mtor[i];
+    }
+    __device__ static bool fits(const OmSceneDev& S) { return S.n_msph <= KS && S.n_mbox <= KB && S.n_mtor <= KT; }
+};
+using MarchedSmall = MarchedRegs<4, 2, 1>;   // S-marched (2, 1, 1), S-full (0, 0, 1)
+
+// for (i < n) body(i): unrolled over the register view's bound, a plain loop otherwise
+template <uint32_t K, class F>
+__device__ __forceinline__ void for_objects(uint32_t n, F body) {
+    if constexpr (K == 0u) {
+        for (uint32_t i = 0; i < n; ++i) body(i);
+    } else {
+#pragma unroll
+        for (uint32_t i = 0; i < K; ++i) if (i < n) body(i);
+    }
+}
+
+// Nearest marched object at p: min |sdf| over the marched objects in type order, strict '<'
+// (the first minimum wins; hits.rs:296-322, 341-358).  An object whose conservative lower
+// bound (om_world.cpp) proves |sdf| > best cannot be the new minimum and is skipped: the
+// result is bit-identical to evaluating every SDF.  -> best (INFINITY if none), kind, index.
+template <class M>
+__device__ __forceinline__ float nearest_marched(const M& m, F3 p, int& bk, uint32_t& bi) {
+    float best = INFINITY;
+    bk = -1; bi = 0;
+    for_objects<M::KS>(m.ns, [&](uint32_t i) {
+        const float v = fabsf(msphere_sdf(m.s[i], p));
+        if (v < best) { best = v; bk = 0; bi = i; }
+    });
+    for_objects<M::KB>(m.nb, [&](uint32_t i) {
+        const OmMBox& B = m.b[i];
+        const float dx = p.x - B.center[0], dy = p.y - B.center[1], dz = p.z - B.center[2];
+        const float thr = (best + B.br) * 1.0001f;                             // inf/NaN -> evaluate
+        if (dx * dx + dy * dy + dz * dz > thr * thr) return;
+        const float v = fabsf(mbox_sdf(B, p));
+        if (v < best) { best = v; bk = 1; bi = i; }
+    });
+    for_objects<M::KT>(m.nt, [&](uint32_t i) {
+        const OmMTorus& T = m.t[i];
+        const float dx = p.x - T.bc[0], dy = p.y - T.bc[1], dz = p.z - T.bc[2];
+        const float thr = best * T.bk + T.br;                                  // inf/NaN -> evaluate
+        if (dx * dx + dy * dy + dz * dz > thr * thr) return;
+        const float v = fabsf(mtorus_sdf(T, p));
+        if (v < best) { best = v; bk = 2; bi = i; }
+    });
+    return best;
+}
+
+// |sdf| of the one marched object (kind, idx) at q.  The register view is only ever indexed
+// by unrolled loop counters (a runtime index would move it to scratch memory).
+template <class M>
+__device__ __forceinline__ float sdf_one(const M& m, int kind, uint32_t idx, F3 q) {
+    if constexpr (M::KS == 0u) {
+        return kind == 0 ? fabsf(msphere_sdf(m.s[idx], q)) : kind == 1 ? fabsf(mbox_sdf(m.b[idx], q)) : fabsf(mtorus_sdf(m.t[idx], q));
+    } else {
+        float v = 0.0f;
+        if (kind == 0) for_objects<M::KS>(m.ns, [&](uint32_t i) { if (i == idx) v = fabsf(msphere_sdf(m.s[i], q)); });
+        else if (kind == 1) for_objects<M::KB>(m.nb, [&](uint32_t i) { if (i == idx) v = fabsf(mbox_sdf(m.b[i], q)); });
+        else for_objects<M::KT>(m.nt, [&](uint32_t i) { if (i == idx) v = fabsf(mtorus_sdf(m.t[i], q)); });
+        return v;
+    }
+}
+
+// unstuck (hits.rs:336-365): the start of the sphere-tracing loop.  Returns false when the
+// world has no marched objects (hits.rs:359); otherwise t is where the march starts.
+template <class M>
+__device__ __forceinline__ bool march_begin(const M& m, F3 o, F3 d, float tmin, float& t) {
     const float HIT = 0.001f;
-    // nearest marched object at r.at(tmin), strict '<' (first minimum wins)
-    F3 p = at(o, d, tmin);
-    float dist = INFINITY; int kind = -1; uint32_t idx = 0;
-    for (uint32_t i = 0; i < S.n_msph; ++i) { const float v = fabsf(msphere_sdf(S.msph[i], p)); if (v < dist) { dist = v; kind = 0; idx = i; } }
-    for (uint32_t i = 0; i < S.n_mbox; ++i) { const float v = fabsf(mbox_sdf(S.mbox[i], p)); if (v < dist) { dist = v; kind = 1; idx = i; } }
-    for (uint32_t i = 0; i < S.n_mtor; ++i) { const float v = fabsf(mtorus_sdf(S.mtor[i], p)); if (v < dist) { dist = v; kind = 2; idx = i; } }
-    if (kind < 0) return -1;                                                   // hits.rs:359
-    float t = tmin;
+    int kind;
+    uint32_t idx;
+    const float dist = nearest_marched(m, at(o, d, tmin), kind, idx);     // r.at(tmin)
+    if (kind < 0) return false;                                                // hits.rs:359
+    t = tmin;
     float aux = dist;
     uint32_t guard = 0;
     while (aux < HIT && guard++ < (1u << 22)) {                                // hits.rs:360-363 (+ safety cap)
         t += HIT / 2.0f;
         const F3 q = at(o, d, t);
-        aux = kind == 0 ? fabsf(msphere_sdf(S.msph[idx], q)) : kind == 1 ? fabsf(mbox_sdf(S.mbox[idx], q)) : fabsf(mtorus_sdf(S.mtor[idx], q));
+        aux = sdf_one(m, kind, idx, q);
     }
+    return true;
+}
+
+// One iteration of the sphere-tracing loop (hits.rs:294-332).  Returns 0 to continue, 1 on
+// a hit (gi = the marched winner's global index, the hit is at t), 2 when the march ends
+// without one.
+template <class M, class Wk>
+__device__ __forceinline__ int march_step(const OmSceneDev& S, const M& m, F3 o, F3 d, float tmax, float closest, float& t,
+                                          uint32_t& iters, int& gi, Wk& w) {
+    const float HIT = 0.001f;
+    if (!(t < tmax && t < closest && iters > 0)) return 2;                    // hits.rs:294
+    iters -= 1;
+    w.add_march();
+    int bk;
+    uint32_t bi;
+    const float best = nearest_marched(m, at(o, d, t), bk, bi);
+    if (bk < 0) return 2;                                                      // hits.rs:323
+    if (best < HIT) {                                                          // hits.rs:325-327
+        gi = (int)(bk == 0 ? S.off_msph + bi : bk == 1 ? S.off_mbox + bi : S.off_mtor + bi);
+        return 1;
+    }
+    t += best;                                                                 // hits.rs:330
+    return 0;
+}
+
+template <class M, class Wk>
+__device__ __forceinline__ int march_with(const OmSceneDev& S, const M& m, F3 o, F3 d, float tmin, float tmax, float closest,
+                                          uint32_t steps, float& t_hit, Wk& w) {
+    float t;
+    if (!march_begin(m, o, d, tmin, t)) return -1;
     uint32_t iters = steps;
-    while (t < tmax && t < closest && iters > 0) {                            // hits.rs:294
-        iters -= 1;
-        w.add_march();
-        p = at(o, d, t);
-        float best = INFINITY; int bk = -1; uint32_t bi = 0;
-        for (uint32_t i = 0; i < S.n_msph; ++i) { const float v = fabsf(msphere_sdf(S.msph[i], p)); if (v < best) { best = v; bk = 0; bi = i; } }
-        for (uint32_t i = 0; i < S.n_mbox; ++i) {
-            const OmMBox& B = S.mbox[i];
-            const float dx = p.x - B.center[0], dy = p.y - B.center[1], dz = p.z - B.center[2];
-            const float thr = (best + B.br) * 1.0001f;                         // inf/NaN -> evaluate
-            if (dx * dx + dy * dy + dz * dz > thr * thr) continue;
-            const float v = fabsf(mbox_sdf(B, p));
-            if (v < best) { best = v; bk = 1; bi = i; }
-        }
-        for (uint32_t i = 0; i < S.n_mtor; ++i) {
-            const OmMTorus& T = S.mtor[i];
-            // conservative cull (om_world.cpp): |sdf| provably > best -> it cannot be the new minimum
-            const float dx = p.x - T.bc[0], dy = p.y - T.bc[1], dz = p.z - T.bc[2];
-            const float thr = best * T.bk + T.br;                              // inf/NaN -> evaluate
-            if (dx * dx + dy * dy + dz * dz > thr * thr) continue;
-            const float v = fabsf(mtorus_sdf(T, p));
-            if (v < best) { best = v; bk = 2; bi = i; }
-        }
-        if (bk < 0) return -1;                                                 // hits.rs:323
-        if (best < HIT) {                                                      // hits.rs:325-327
-            t_hit = t;
-            return (int)(bk == 0 ? S.off_msph + bi : bk == 1 ? S.off_mbox + bi : S.off_mtor + bi);
-        }
-        t += best;                                                             // hits.rs:330
-    }
+    int gi = -1, r;
+    while ((r = march_step(S, m, o, d, tmax, closest, t, iters, gi, w)) == 0) {}
+    if (r == 1) { t_hit = t; return gi; }
     return -1;
+}
+
+// unstuck + sphere-tracing loop (hits.rs:287-365).  Returns the marched winner's global
+// index or -1; `t_hit` receives the hit t.  Small marched sets (every reference scene) are
+// copied to registers once per call instead of reloaded at every step.
+template <class Wk>
+__device__ __forceinline__ int march(const OmSceneDev& S, F3 o, F3 d, float tmin, float tmax, float closest,
+                                     uint32_t steps, float& t_hit, Wk& w) {
+#ifndef OM_MARCH_ARRAYS_ONLY
+    if (MarchedSmall::fits(S)) return march_with(S, MarchedSmall(S), o, d, tmin, tmax, closest, steps, t_hit, w);
+#endif
+    return march_with(S, MarchedArrays(S), o, d, tmin, tmax, closest, steps, t_hit, w);
 }
 
 // Build the HitRecord of the winner (point, normal) — the winner's own exact

@@ -18,6 +18,7 @@ struct QueueSet {
     float4* res = nullptr;       // colour.xyz, depth
     uint32_t* res_id = nullptr;  // obj id (0xFFFFFFFF = no sample)
     uint32_t* counts = nullptr;  // per bounce, per queue segment: live rays
+    float2* hit = nullptr;       // split march pipeline: (closest, winner) per queue slot
     void release();
 };
 

@@ -40,7 +40,8 @@ void QueueSet::release() {
     if (res) (void)hipFree(res);
     if (res_id) (void)hipFree(res_id);
     if (counts) (void)hipFree(counts);
-    res = nullptr; res_id = nullptr; counts = nullptr;
+    if (hit) (void)hipFree(hit);
+    res = nullptr; res_id = nullptr; counts = nullptr; hit = nullptr;
 }
 
 void Buffers::release() {
@@ -106,6 +107,23 @@ constexpr uint32_t kTailDefault = 16;                             // first bounc
 __host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
     return S.b2_lds_bytes ? 0u : (S.n_b2nodes < OM_WF_HYB_BYTES / 64u ? S.n_b2nodes : OM_WF_HYB_BYTES / 64u);
 }
+// Worlds with marched primitives: 1 (default) runs each bounce as a lane-refilling march
+// launch (k_march: every lane takes the segment's next path as soon as its march ends, so a
+// wave no longer waits for its longest march) followed by the shade+compact launch reading
+// the (closest, winner) it wrote; 0 keeps the fused trace+march+shade bounce kernel.
+#ifndef OM_WF_MARCH_SPLIT
+#define OM_WF_MARCH_SPLIT 1
+#endif
+// k_march keeps a small marched set (MarchedSmall) in registers (1) or reads the scene arrays
+// (0, default: the second copy of the march code doubles the kernel and it measured 12% slower
+// on C2, 1437-1451 vs 1624-1639 Msamples/s).
+#ifndef OM_WF_MARCH_REGS
+#define OM_WF_MARCH_REGS 0
+#endif
+// k_march refills its idle lanes once at least this many of a wave's 64 wait.
+#ifndef OM_WF_REFILL
+#define OM_WF_REFILL 16
+#endif
 // Queue segments (= bounce workgroups) per CU: OM_WF_LANES_PER_CU / OM_WF_BLOCK.
 #ifndef OM_WF_LANES_PER_CU
 #define OM_WF_LANES_PER_CU 4096
@@ -303,14 +321,48 @@ __device__ __forceinline__ bool shade_path(const OmSceneDev& S, const OmParamsDe
     return true;
 }
 
+// Camera sample i of the batch (render_thread.rs:176-192): -> p (a fresh path) and its
+// pixel; false (and no sample recorded in res_id) when the sample is not taken.
+__device__ __forceinline__ bool gen_path(const OmParamsDev& P, const Gen& R, uint64_t i, Path& p, uint32_t& pixel,
+                                         uint32_t* __restrict__ res_id) {
+    const uint32_t s_local = (uint32_t)(i / R.n_pixels), k = (uint32_t)(i - (uint64_t)s_local * R.n_pixels);
+    pixel = R.pixels[k];
+    // the sample index is the pixel's Stats.n (jitters[pixel.stats.n], render_thread.rs:188).
+    // Fixed-spp calls take it from the call-start snapshot plus the samples of earlier
+    // batches, so a batch never waits for the previous batch's accumulate; adaptive
+    // calls (one sample per batch) read the live Stats for n and the done flag.
+    uint32_t s;
+    bool live;
+    if (R.n0) {
+        s = R.n0[k] + R.done + s_local;
+        live = s < P.spp_total;
+    } else {
+        const om_pixel_stats& ps = R.stats[R.by_pixel ? pixel : k];
+        s = ps.n + s_local;
+        live = s < P.spp_total && !(P.adaptive && (ps.flags & 1u));
+    }
+    if (!live) {
+        res_id[i] = kNoSample;
+        return false;
+    }
+    p.g = path_rng(P.skey, pixel, s);
+    const uint32_t line = pixel / P.width;
+    gen_camera_ray(R.C, P, R.jitter, (float)(pixel - P.width * line), (float)line, s, p.g, p.o, p.d);
+    p.cur = f3(1.0f, 1.0f, 1.0f); p.depthf = 0.0f; p.first_id = 0u; p.seg = 0u; p.slot = (uint32_t)i;
+    return true;
+}
+
 // ---------------------------------------------------------------- bounce
 // Workgroup s: the paths of segment s of queue `in` (FIRST: the camera samples
 // [s*segcap, (s+1)*segcap) of the batch) -> survivors into segment s of `out`.
-template <int TR, bool COUNT, bool MARCH, bool FIRST>
+// HIT (split march pipeline): no trace here; the (closest, winner) of every path of the
+// segment was written to `hitbuf` (queue-slot order) by k_march.
+template <int TR, bool COUNT, bool MARCH, bool FIRST, bool HIT = false>
 __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmParamsDev P, Seg G, Gen R, Queue in,
                                                  const uint32_t* __restrict__ count_in, Queue out,
                                                  uint32_t* __restrict__ count_out, float4* __restrict__ res,
-                                                 uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters) {
+                                                 uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters,
+                                                 const float2* __restrict__ hitbuf) {
     const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
     uint32_t n;
     if (FIRST) {
@@ -328,7 +380,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
     if (threadIdx.x == 0) { q_next = kBlk / 64u; q_out = 0u; }
     __syncthreads();
 #endif
-    const Tracer T = stage_scene<TR>(S);
+    const Tracer T = HIT ? Tracer{} : stage_scene<TR>(S);
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
     WorkT<COUNT> w;
     uint32_t segs = 0, run = 0;
@@ -347,37 +399,17 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
             const uint64_t i = seg0 + jj;
             bool live = true;
             if (FIRST) {
-                const uint32_t s_local = (uint32_t)(i / R.n_pixels), k = (uint32_t)(i - (uint64_t)s_local * R.n_pixels);
-                const uint32_t pixel = R.pixels[k];
-                p_pixel = pixel;
-                // the sample index is the pixel's Stats.n (jitters[pixel.stats.n], render_thread.rs:188).
-                // Fixed-spp calls take it from the call-start snapshot plus the samples of earlier
-                // batches, so a batch never waits for the previous batch's accumulate; adaptive
-                // calls (one sample per batch) read the live Stats for n and the done flag.
-                uint32_t s;
-                if (R.n0) {
-                    s = R.n0[k] + R.done + s_local;
-                    live = s < P.spp_total;
-                } else {
-                    const om_pixel_stats& ps = R.stats[R.by_pixel ? pixel : k];
-                    s = ps.n + s_local;
-                    live = s < P.spp_total && !(P.adaptive && (ps.flags & 1u));
-                }
-                if (live) {
-                    p.g = path_rng(P.skey, pixel, s);
-                    const uint32_t line = pixel / P.width;
-                    gen_camera_ray(R.C, P, R.jitter, (float)(pixel - P.width * line), (float)line, s, p.g, p.o, p.d);
-                    p.cur = f3(1.0f, 1.0f, 1.0f); p.depthf = 0.0f; p.first_id = 0u; p.seg = 0u; p.slot = (uint32_t)i;
-                } else {
-                    res_id[i] = kNoSample;
-                }
+                live = gen_path(P, R, i, p, p_pixel, res_id);
             } else {
                 load_ray(in, i, p);
             }
             if (live) {
                 float closest;
                 int best;
-                if (FIRST && (TR == TR_BVH2_LDS || TR == TR_BVH2_GLOBAL) && R.tile_off) {
+                if (HIT) {
+                    const float2 h = hitbuf[i];
+                    closest = h.x; best = __float_as_int(h.y);
+                } else if (FIRST && (TR == TR_BVH2_LDS || TR == TR_BVH2_GLOBAL) && R.tile_off) {
                     const uint32_t line = p_pixel / P.width;
                     const uint32_t tile = (p_pixel - line * P.width) / 8u + (line / 8u) * P.tiles_x;
                     closest = P.tmax;
@@ -434,6 +466,106 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
     if (threadIdx.x == 0) count_out[blockIdx.x] = run;
     if (COUNT) {
         flush_counter(counters, OMC_SEGMENTS, segs);
+        flush_counter(counters, OMC_PRIM_TESTS, w.prim);
+        flush_counter(counters, OMC_PRE_TESTS, w.pre);
+        flush_counter(counters, OMC_MARCH, w.march);
+    }
+}
+
+// ---------------------------------------------------------------- split march pipeline
+// k_raygen: the camera samples [s*segcap, (s+1)*segcap) of the batch; the taken ones are
+// compacted into segment s of `out` (bounce 0 of the split pipeline reads them from there).
+template <bool COUNT>
+__global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_raygen(OmParamsDev P, Seg G, Gen R, Queue out,
+                                                 uint32_t* __restrict__ count_out, uint32_t* __restrict__ res_id) {
+    const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
+    const uint64_t paths = (uint64_t)R.n_pixels * R.batch;
+    const uint32_t n = seg0 < paths ? (uint32_t)std::min<uint64_t>(G.segcap, paths - seg0) : 0u;
+    __shared__ uint32_t q_out;
+    if (threadIdx.x == 0) q_out = 0u;
+    __syncthreads();
+    const uint32_t lane = __lane_id();
+    for (uint32_t base = 0; base < n; base += kBlk) {
+        const uint32_t jj = base + threadIdx.x;
+        Path p;
+        uint32_t pixel;
+        const bool keep = jj < n && gen_path(P, R, seg0 + jj, p, pixel, res_id);
+        const uint64_t m = __ballot(keep);
+        uint32_t obase = 0u;
+        if (lane == 0 && m) obase = atomicAdd(&q_out, (uint32_t)__popcll(m));
+        obase = __builtin_amdgcn_readfirstlane(obase);
+        if (keep) store_path(out, seg0 + obase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), p);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) count_out[blockIdx.x] = q_out;
+}
+
+// k_march: closest traced hit + unstuck + sphere tracing (hits.rs:270-365) of every path of
+// segment s of `in`, with LANE REFILL: a lane whose march ends writes (closest, winner) to
+// hit[slot] and waits until OM_WF_REFILL lanes of its wave are idle; they then take the
+// segment's next paths together (wave-aggregated LDS counter).  The wave's march iterations
+// are then no longer the max over 64 paths' step counts.
+template <int TR, bool COUNT, class M, class Wk>
+__device__ __forceinline__ void march_lanes(const OmSceneDev& S, const OmParamsDev& P, const Tracer& T, const M& m,
+                                            const Queue& in, uint64_t seg0, uint32_t n, uint32_t& next,
+                                            float2* __restrict__ hit, Wk& w) {
+    const uint32_t lane = __lane_id();
+    uint32_t j = threadIdx.x;
+    bool act = j < n, marching = false;
+    bool dry = !act;                                   // the segment has no path left for this lane
+    F3 o = f3(0.0f, 0.0f, 0.0f), d = o;
+    float t = 0.0f, closest = 0.0f;
+    int best = -1;
+    uint32_t iters = 0;
+    auto start = [&]() {
+        const float4 a = in.q0[seg0 + j], b = in.q1[seg0 + j];
+        o = f3(a.x, a.y, a.z); d = f3(b.x, b.y, b.z);
+        best = trace<TR, false>(S, P, T, o, d, closest, w);
+        marching = march_begin(m, o, d, P.tmin, t);
+        iters = P.march_steps;
+    };
+    if (act) start();
+    for (;;) {
+        if (act) {
+            int gi = -1;
+            const int r = marching ? march_step(S, m, o, d, P.tmax, closest, t, iters, gi, w) : 2;
+            if (r != 0) {
+                if (r == 1) { best = gi; closest = t; }
+                hit[seg0 + j] = make_float2(closest, __int_as_float(best));
+                act = false;
+            }
+        }
+        // refill the idle lanes together once enough of them wait (or nothing else runs):
+        // a refill runs the trace and unstuck, which costs several march steps
+        const uint64_t want = __ballot(!act && !dry), busy = __ballot(act);
+        if (want && (__popcll(want) >= OM_WF_REFILL || busy == 0)) {
+            uint32_t base = 0u;
+            if (lane == 0) base = atomicAdd(&next, (uint32_t)__popcll(want));
+            base = __builtin_amdgcn_readfirstlane(base);
+            if (!act && !dry) {
+                j = base + (uint32_t)__popcll(want & ((1ull << lane) - 1ull));
+                if (j < n) { act = true; start(); } else dry = true;
+            }
+        }
+        if (__ballot(act) == 0) break;
+    }
+}
+
+template <int TR, bool COUNT>
+__global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_march(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
+                                                const uint32_t* __restrict__ count_in, float2* __restrict__ hit,
+                                                unsigned long long* __restrict__ counters) {
+    const uint32_t n = count_in[blockIdx.x];
+    if (n == 0) return;
+    const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
+    __shared__ uint32_t next;
+    if (threadIdx.x == 0) next = kBlk;
+    __syncthreads();
+    const Tracer T = stage_scene<TR>(S);
+    WorkT<COUNT> w;
+    if (OM_WF_MARCH_REGS && MarchedSmall::fits(S)) march_lanes<TR, COUNT>(S, P, T, MarchedSmall(S), in, seg0, n, next, hit, w);
+    else march_lanes<TR, COUNT>(S, P, T, MarchedArrays(S), in, seg0, n, next, hit, w);
+    if (COUNT) {
         flush_counter(counters, OMC_PRIM_TESTS, w.prim);
         flush_counter(counters, OMC_PRE_TESTS, w.pre);
         flush_counter(counters, OMC_MARCH, w.march);
@@ -548,6 +680,7 @@ hipError_t grow(Buffers& B, uint64_t cap, uint32_t counts_n, int nsets) {
             }
             if ((e = hipMalloc(&S.res, cap * sizeof(float4))) != hipSuccess) return e;
             if ((e = hipMalloc(&S.res_id, cap * sizeof(uint32_t))) != hipSuccess) return e;
+            if ((e = hipMalloc(&S.hit, cap * sizeof(float2))) != hipSuccess) return e;
         }
         B.cap = cap; B.nsets = nsets;
     }
@@ -573,6 +706,37 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
     Timer& tm = *L.timer;
     const bool each = tm.mode == 1;
     uint32_t launches = 0;
+    if (MARCH && OM_WF_MARCH_SPLIT) {
+        {
+            const int ti = each ? tm.begin(st) : -1;
+            hipLaunchKernelGGL((k_raygen<COUNT>), dim3(G.nseg), dim3(kBlk), 0, st, L.P, G, R, queue(B, 0), B.counts, B.res_id);
+            tm.end(ti, OM_KT_BOUNCE0, st);
+            ++launches;
+        }
+        for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
+            const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
+            const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
+            if (bounce > 0 && bounce >= tail_at) {
+                const uint32_t grid = (G.nseg + kTailSpb - 1u) / kTailSpb;
+                const int ti = each ? tm.begin(st) : -1;
+                hipLaunchKernelGGL((k_tail<TR, COUNT, MARCH>), dim3(grid), dim3(kBlk), lds, st, L.S, L.P, G, in, cin,
+                                   B.res, B.res_id, L.counters);
+                tm.end(ti, OM_KT_TAIL, st);
+                return launches + 1u;
+            }
+            uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
+            const int kc = bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE;
+            int ti = each ? tm.begin(st) : -1;
+            hipLaunchKernelGGL((k_march<TR, COUNT>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin, B.hit, L.counters);
+            tm.end(ti, kc, st);
+            ti = each ? tm.begin(st) : -1;
+            hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false, true>), dim3(G.nseg), dim3(kBlk), 0, st, L.S, L.P, G, R, in,
+                               cin, out, cout, B.res, B.res_id, L.counters, (const float2*)B.hit);
+            tm.end(ti, kc, st);
+            launches += 2u;
+        }
+        return launches;
+    }
     for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
         const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
         const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
@@ -588,10 +752,10 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         const int ti = each ? tm.begin(st) : -1;
         if (bounce == 0)
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, true>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
-                               cin, out, cout, B.res, B.res_id, L.counters);
+                               cin, out, cout, B.res, B.res_id, L.counters, (const float2*)nullptr);
         else
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
-                               cin, out, cout, B.res, B.res_id, L.counters);
+                               cin, out, cout, B.res, B.res_id, L.counters, (const float2*)nullptr);
         tm.end(ti, bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE, st);
         ++launches;
     }

@@ -38,6 +38,14 @@ declare -A V=(
   [hyb0]="$COMMON $DEV -DOM_WF_HYB_BYTES=0"
   [hyb16k]="$COMMON $DEV -DOM_WF_HYB_BYTES=16384"
   [hyb40k]="$COMMON $DEV -DOM_WF_HYB_BYTES=40960"
+  # marched worlds: the fused trace+march+shade bounce kernel instead of k_march + shade
+  [msplit0]="$COMMON $DEV -DOM_WF_MARCH_SPLIT=0"
+  [mregs1]="$COMMON $DEV -DOM_WF_MARCH_REGS=1"
+  [marrays]="$COMMON $DEV -DOM_MARCH_ARRAYS_ONLY"
+  [refill8]="$COMMON $DEV -DOM_WF_REFILL=8"
+  [refill16]="$COMMON $DEV -DOM_WF_REFILL=16"
+  [refill48]="$COMMON $DEV -DOM_WF_REFILL=48"
+  [refill64]="$COMMON $DEV -DOM_WF_REFILL=64"
   [lpc2k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=2048"
   [lpc8k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=8192"
   [lpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=16384"
