@@ -181,7 +181,7 @@ __global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(O
         float seg_depth; uint32_t seg_id;
         if (best >= 0) {
             F3 point, normal;
-            finalize(S, best, o, d, P.tmin, closest, point, normal);
+            finalize<MARCH>(S, best, o, d, P.tmin, closest, point, normal);
             F3 nd, att;
             scatter(S.mats[best], d, normal, g, nd, att);
             cur = mul(cur, att);

@@ -401,6 +401,9 @@ __device__ __forceinline__ int march(const OmSceneDev& S, F3 o, F3 d, float tmin
 
 // Build the HitRecord of the winner (point, normal) — the winner's own exact
 // test re-run with tmax = its root reproduces the same root bit for bit.
+// MARCH = false (worlds without marched primitives, a compile-time split like the trace's):
+// the marched winners' normal code (central differences, ~60 sqrt/div) is left out.
+template <bool MARCH = true>
 __device__ __forceinline__ void finalize(const OmSceneDev& S, int gi, F3 o, F3 d, float tmin, float t, F3& point, F3& normal) {
     const uint32_t g = (uint32_t)gi;
     if (g < S.off_tri) {                                                       // Sphere / Cube
@@ -435,6 +438,7 @@ __device__ __forceinline__ void finalize(const OmSceneDev& S, int gi, F3 o, F3 d
         return;
     }
     point = at(o, d, t);                                                       // marched (hits.rs:326)
+    if (!MARCH) { normal = f3(0.0f, 0.0f, 0.0f); return; }                    // unreachable: no marched winner
     if (g < S.off_mbox) normal = msphere_normal(S.msph[g - S.off_msph], point);
     else if (g < S.off_mtor) normal = mbox_normal(S.mbox[g - S.off_mbox], point);
     else normal = mtorus_normal(S.mtor[g - S.off_mtor], point);

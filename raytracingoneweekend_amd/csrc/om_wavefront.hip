@@ -283,13 +283,14 @@ __device__ __forceinline__ int trace(const OmSceneDev& S, const OmParamsDev& P, 
 // handle_hit + ray_color's termination rules (render_thread.rs:105-143) for one
 // segment.  Returns true when the path continues (p advanced to the next segment);
 // otherwise the sample's (colour, depth, id) is written to its result slot.
+template <bool MARCH>
 __device__ __forceinline__ bool shade_path(const OmSceneDev& S, const OmParamsDev& P, uint32_t depth_cap, Path& p,
                                            float closest, int best, float4* __restrict__ res,
                                            uint32_t* __restrict__ res_id) {
     float seg_depth; uint32_t seg_id;
     if (best >= 0) {                                                   // handle_hit, Some(hr)
         F3 point, normal;
-        finalize(S, best, p.o, p.d, P.tmin, closest, point, normal);
+        finalize<MARCH>(S, best, p.o, p.d, P.tmin, closest, point, normal);
         F3 nd, att;
         scatter(S.mats[best], p.d, normal, p.g, nd, att);
         p.cur = mul(p.cur, att);
@@ -436,10 +437,10 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
                 {
                     Path p2 = p;
                     p2.cur.x *= P.march_steps == 0xDEADBEEFu ? 2.0f : 1.0f;
-                    if (shade_path(S, P, depth_cap, p2, closest, best, res, res_id) && p2.seg == 0xFFFFFFu) res_id[1] = 0u;
+                    if (shade_path<MARCH>(S, P, depth_cap, p2, closest, best, res, res_id) && p2.seg == 0xFFFFFFu) res_id[1] = 0u;
                 }
 #endif
-                keep = shade_path(S, P, depth_cap, p, closest, best, res, res_id);
+                keep = shade_path<MARCH>(S, P, depth_cap, p, closest, best, res, res_id);
                 if (COUNT) segs++;
             }
         }
@@ -609,7 +610,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmPar
             float closest;
             const int best = trace<TR, MARCH>(S, P, T, p.o, p.d, closest, w);
             if (COUNT) segs++;
-            if (!shade_path(S, P, depth_cap, p, closest, best, res, res_id)) break;
+            if (!shade_path<MARCH>(S, P, depth_cap, p, closest, best, res, res_id)) break;
         }
     }
     if (COUNT) {
