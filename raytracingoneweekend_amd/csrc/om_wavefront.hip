@@ -114,9 +114,11 @@ __host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
 #ifndef OM_WF_MARCH_SPLIT
 #define OM_WF_MARCH_SPLIT 1
 #endif
-// k_march keeps a small marched set (MarchedSmall) in registers (1) or reads the scene arrays
-// (0, default: the second copy of the march code doubles the kernel and it measured 12% slower
-// on C2, 1437-1451 vs 1624-1639 Msamples/s).
+// k_march instances: SMALL = keep a marched set that fits MarchedSmall in registers (chosen on
+// the host, one copy of the march code per instance) instead of reading the scene arrays.
+// Off by default: on C2 the register instance measured 1419-1454 Msamples/s against 1618-1624
+// for the arrays (one instance holding both views: 1437-1451), although the same view speeds
+// up the megakernel's march() (983 -> 1080).
 #ifndef OM_WF_MARCH_REGS
 #define OM_WF_MARCH_REGS 0
 #endif
@@ -552,7 +554,7 @@ __device__ __forceinline__ void march_lanes(const OmSceneDev& S, const OmParamsD
     }
 }
 
-template <int TR, bool COUNT>
+template <int TR, bool COUNT, bool SMALL>
 __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_march(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
                                                 const uint32_t* __restrict__ count_in, float2* __restrict__ hit,
                                                 unsigned long long* __restrict__ counters) {
@@ -564,7 +566,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_march(OmSceneDev S, OmPa
     __syncthreads();
     const Tracer T = stage_scene<TR>(S);
     WorkT<COUNT> w;
-    if (OM_WF_MARCH_REGS && MarchedSmall::fits(S)) march_lanes<TR, COUNT>(S, P, T, MarchedSmall(S), in, seg0, n, next, hit, w);
+    if constexpr (SMALL) march_lanes<TR, COUNT>(S, P, T, MarchedSmall(S), in, seg0, n, next, hit, w);
     else march_lanes<TR, COUNT>(S, P, T, MarchedArrays(S), in, seg0, n, next, hit, w);
     if (COUNT) {
         flush_counter(counters, OMC_PRIM_TESTS, w.prim);
@@ -728,7 +730,12 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
             uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
             const int kc = bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE;
             int ti = each ? tm.begin(st) : -1;
-            hipLaunchKernelGGL((k_march<TR, COUNT>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin, B.hit, L.counters);
+            const bool small = OM_WF_MARCH_REGS && L.S.n_msph <= MarchedSmall::KS && L.S.n_mbox <= MarchedSmall::KB &&
+                               L.S.n_mtor <= MarchedSmall::KT;
+            if (small)
+                hipLaunchKernelGGL((k_march<TR, COUNT, true>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin, B.hit, L.counters);
+            else
+                hipLaunchKernelGGL((k_march<TR, COUNT, false>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin, B.hit, L.counters);
             tm.end(ti, kc, st);
             ti = each ? tm.begin(st) : -1;
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false, true>), dim3(G.nseg), dim3(kBlk), 0, st, L.S, L.P, G, R, in,

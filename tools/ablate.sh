@@ -40,8 +40,8 @@ declare -A V=(
   [hyb40k]="$COMMON $DEV -DOM_WF_HYB_BYTES=40960"
   # marched worlds: the fused trace+march+shade bounce kernel instead of k_march + shade
   [msplit0]="$COMMON $DEV -DOM_WF_MARCH_SPLIT=0"
-  [mregs1]="$COMMON $DEV -DOM_WF_MARCH_REGS=1"
   [marrays]="$COMMON $DEV -DOM_MARCH_ARRAYS_ONLY"
+  [mregs1]="$COMMON $DEV -DOM_WF_MARCH_REGS=1"
   [refill8]="$COMMON $DEV -DOM_WF_REFILL=8"
   [refill16]="$COMMON $DEV -DOM_WF_REFILL=16"
   [refill48]="$COMMON $DEV -DOM_WF_REFILL=48"
