@@ -35,12 +35,16 @@ from raytracingoneweekend_amd import shard  # noqa: E402
 
 W, H, MAX_DEPTH, TMIN, TMAX, SEED, SCENE_SEED = 1920, 1080, 50, 0.001, 100.0, 1, 0x5EED
 SPP_PER_STEP = 32
-# BASELINE.json configs: C1 is the metric's workload (the default line); C2/C3 are measured
-# with --config for DESIGN.md (the marched SDF scene at 256 march steps, the 10k-sphere BVH).
+# BASELINE.json configs: C1 is the metric's workload (the default line); C2/C3/C4 are measured
+# with --config for DESIGN.md (the marched SDF scene at 256 march steps, the 10k-sphere BVH,
+# the 4K frame of the multi-GPU config).
 CONFIGS = {
     "C1": {"scene": "S-traced", "spp": 512, "march_steps": 1024},
     "C2": {"scene": "S-marched", "spp": 256, "march_steps": 256},
     "C3": {"scene": "S-10k", "spp": 256, "march_steps": 1024},
+    # the multi-GPU config (BASELINE.json configs[4]: 3840x2160, 4096 spp, 8 GPUs); weak scaling
+    # as for C1: each rank renders its 1/N of the tiles at spp_per_step * N per step
+    "C4": {"scene": "S-traced", "spp": 4096, "march_steps": 1024, "size": (3840, 2160)},
 }
 
 
@@ -119,8 +123,10 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0)
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
+    global W, H
+    W, H = cfg.get("size", (W, H))
     if args.steps is None:
-        args.steps = cfg["spp"] // args.spp_per_step
+        args.steps = cfg["spp"] // (args.spp_per_step * args.gpus) if args.config == "C4" else cfg["spp"] // args.spp_per_step
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -289,7 +295,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "C4" else "weak",   # C4: the fixed 4K x 4096-spp frame
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic: {cfg['scene']} (om-rng scene seed 0x5EED), render seed 1",
