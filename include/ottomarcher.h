@@ -202,12 +202,13 @@ om_status om_reset_counters(om_ctx* ctx, void* stream);
 om_status om_set_counting(om_ctx* ctx, int32_t enable);
 /* Execution pipeline (all bit-identical):
  *   OM_PIPELINE_WAVEFRONT  per bounce one {trace -> shade -> compact} launch over SoA path
- *                          queues in HBM (bounce 0 generates the camera rays), then one
- *                          persistent tail launch, then accumulate
+ *                          queues in HBM (bounce 0 generates the camera rays; marched worlds:
+ *                          a lane-refilling march launch, then shade), then one persistent
+ *                          tail launch, then accumulate
  *   OM_PIPELINE_MEGAKERNEL one persistent-path kernel per call
  *   OM_PIPELINE_AUTO       (default) the faster one measured for the call: megakernel for
- *                          adaptive renders and for worlds with marched primitives when
- *                          om_set_streams is 1, else wavefront */
+ *                          worlds with marched primitives when batches run serially
+ *                          (adaptive calls, or om_set_streams 1), else wavefront */
 enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1, OM_PIPELINE_AUTO = 2 };
 om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
 /* Wavefront pipeline: bounces >= `bounce` are finished by one persistent tail launch

@@ -442,13 +442,13 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     }
     if (threads == 0) return OM_OK;
     int pipeline = c->pipeline;
-    // AUTO: the measured faster pipeline: the megakernel for adaptive sampling
-    // (one sample per pixel per wavefront pass; C1 adaptive: 2804 vs 553 credited Msamples/s)
-    // and for marched SDFs when batches run serially (C2: 916 vs 790); else the wavefront
-    // (C2 with concurrent batches: 1111 vs 976, C1: 5722 vs 3142).
+    // AUTO: the measured faster pipeline: the megakernel for marched SDFs when
+    // batches run serially (adaptive calls, or om_set_streams(1); C2: 916 vs 790); else the
+    // wavefront (C2 with concurrent batches: 1625 vs 1080, C1: 6100 vs 3142, C1 adaptive with
+    // 16-sample speculative batches: 3190 vs 2749 credited Msamples/s).
     if (pipeline == OM_PIPELINE_AUTO) {
         const bool marched = (c->scene.n_msph + c->scene.n_mbox + c->scene.n_mtor) != 0;
-        pipeline = (p->adaptive || (marched && c->wf_streams < 2)) ? OM_PIPELINE_MEGAKERNEL : OM_PIPELINE_WAVEFRONT;
+        pipeline = (marched && (p->adaptive || c->wf_streams < 2)) ? OM_PIPELINE_MEGAKERNEL : OM_PIPELINE_WAVEFRONT;
     }
     int mode = c->kernel;
     if (mode == OM_KERNEL_AUTO) mode = OM_KERNEL_BVH2;

@@ -126,6 +126,14 @@ __host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
 #ifndef OM_WF_REFILL
 #define OM_WF_REFILL 16
 #endif
+// Adaptive calls: samples per pixel per (serial) batch.  Bounce 0 reads each pixel's retirement
+// flag at the batch start; a pixel that retires inside a batch has its remaining samples of
+// that batch rendered and dropped by k_accumulate (the result is the sequential one).  C1
+// adaptive, 16 spp per call (tools/adaptive_sweep.sh): 1 / 4 / 8 / 16 -> 564 / 1519 / 2376 /
+// 3190 credited Msamples/s (megakernel: 2749).
+#ifndef OM_WF_ADAPTIVE_BATCH
+#define OM_WF_ADAPTIVE_BATCH 16
+#endif
 // Queue segments (= bounce workgroups) per CU: OM_WF_LANES_PER_CU / OM_WF_BLOCK.
 #ifndef OM_WF_LANES_PER_CU
 #define OM_WF_LANES_PER_CU 4096
@@ -333,7 +341,7 @@ __device__ __forceinline__ bool gen_path(const OmParamsDev& P, const Gen& R, uin
     // the sample index is the pixel's Stats.n (jitters[pixel.stats.n], render_thread.rs:188).
     // Fixed-spp calls take it from the call-start snapshot plus the samples of earlier
     // batches, so a batch never waits for the previous batch's accumulate; adaptive
-    // calls (one sample per batch) read the live Stats for n and the done flag.
+    // calls (serial batches) read the live Stats for n and the done flag.
     uint32_t s;
     bool live;
     if (R.n0) {
@@ -640,6 +648,10 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
         st.avg_depth = in.avg_depth; st.bad = in.bad_avgs;
         st.rgbf = (uint32_t)in.color[0] | ((uint32_t)in.color[1] << 8) | ((uint32_t)in.color[2] << 16) | ((uint32_t)in.flags << 24);
         for (uint32_t s = 0; s < batch; ++s) {                                 // sample order == reference order
+            // adaptive batches of several samples: a pixel that retires at sample j takes no more
+            // (ThreadPixels::add_run, render_thread.rs:68-102); the batch's later samples of it
+            // were rendered speculatively and are dropped here
+            if (P.adaptive && (st.rgbf & 0x01000000u)) break;
             const uint64_t t = (uint64_t)s * n_pixels + k;
             const uint32_t id = res_id[t];
             if (id == kNoSample) continue;
@@ -810,7 +822,8 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     const uint64_t kMaxPaths = 1ull << 25;   // 33.5M paths per batch (~4.9 GB of queues per set)
     const uint32_t want = std::max<uint32_t>(1u, std::min<uint32_t>(L.streams, (uint32_t)kMaxSets));
     const bool concurrent = !L.P.adaptive && want >= 2u && L.P.sample_count >= 2u;
-    uint32_t batch = L.P.adaptive ? 1u : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));
+    uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));
+    if (L.P.adaptive) batch = std::min<uint32_t>(batch, OM_WF_ADAPTIVE_BATCH);
     if (concurrent) batch = std::min<uint32_t>(batch, (L.P.sample_count + want - 1u) / want);
     const uint32_t nb = (L.P.sample_count + batch - 1u) / batch;
     const uint32_t ns = concurrent ? std::min<uint32_t>(want, nb) : 1u;

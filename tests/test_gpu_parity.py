@@ -76,6 +76,25 @@ def test_adaptive_retirement_bit_exact(om, oracle, pipeline):
     assert got["n"].min() < SPP  # some pixels (sky) retired early, like the reference
 
 
+@pytest.mark.parametrize("sample_count", [1, 5, 24])
+def test_adaptive_speculative_batches_bit_exact(om, oracle, sample_count):
+    """Wavefront adaptive calls render up to 16 samples per pixel per batch and drop those
+    past a pixel's retirement: progressive calls of 1 / 5 / 24 samples ==
+    the sequential oracle, on a frame bigger than one workgroup's segment."""
+    W, H, SPP = 72, 40, 24
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam, pipeline="wavefront")
+    pix = om.PixelsBox.new(W * H)
+    for _ in range((SPP + sample_count - 1) // sample_count):
+        om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=13, adaptive=True, sample_count=sample_count)
+    exp, _ = oracle.render(oracle.random_scene(0x5EED), oracle.default_camera(W / H),
+                           oracle.params(W, H, SPP, seed=13, adaptive=True))
+    nb, msg = compare_stats(pix.pixels, exp, f"adaptive/{sample_count}")
+    assert nb == 0, msg
+    assert pix.pixels["n"].min() < SPP
+
+
 @pytest.mark.parametrize("pipeline", PIPELINES)
 def test_progressive_calls_equal_single_call(om, pipeline):
     W, H = 40, 24
@@ -193,16 +212,17 @@ def test_tail_bounce_is_bit_identical(om, oracle, tail):
 
 
 def test_auto_pipeline_choice(om, oracle):
-    """OM_PIPELINE_AUTO: the megakernel for adaptive renders and for marched SDFs with serial
-    batches, the wavefront otherwise (the faster one measured on C1 / C2),
-    observed through the per-launch timing classes; bit-exact."""
+    """OM_PIPELINE_AUTO: the megakernel for marched SDFs with serial batches (adaptive or one
+    stream), the wavefront otherwise (the faster one measured on C1 / C2 / C1 adaptive,
+    DESIGN.md §5.8), observed through the per-launch timing classes; bit-exact."""
     import ctypes as C
     from raytracingoneweekend_amd import _lib as L
     W, H = 24, 16
     for world, oworld, adaptive, streams, want in (
             (om.marched_scene(), oracle.marched_scene(), False, 1, "megakernel"),
             (om.marched_scene(), oracle.marched_scene(), False, 2, "bounce0"),
-            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), True, 2, "megakernel"),
+            (om.marched_scene(), oracle.marched_scene(), True, 2, "megakernel"),
+            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), True, 2, "bounce0"),
             (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, 1, "bounce0"),
             (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, 2, "bounce0")):
         cam = om.default_camera(W / H)

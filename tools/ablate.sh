@@ -46,6 +46,10 @@ declare -A V=(
   [refill16]="$COMMON $DEV -DOM_WF_REFILL=16"
   [refill48]="$COMMON $DEV -DOM_WF_REFILL=48"
   [refill64]="$COMMON $DEV -DOM_WF_REFILL=64"
+  # adaptive wavefront: samples per pixel per serial batch
+  [ab1]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=1"
+  [ab4]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=4"
+  [ab16]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=16"
   [lpc2k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=2048"
   [lpc8k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=8192"
   [lpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=16384"
