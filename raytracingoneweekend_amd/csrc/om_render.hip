@@ -353,7 +353,7 @@ om_status validate(om_ctx* c, const om_camera* cam, const om_render_params* p) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
     if (!cam || !p) return set_err(c, OM_ERR_INVALID, "null camera/params");
     if (!c->have_world) return set_err(c, OM_ERR_STATE, "om_upload_world must precede rendering");
-    if (p->width < 2 || p->height < 2) return set_err(c, OM_ERR_INVALID, "width/height must be >= 2");
+    if (p->width == 0 || p->height == 0) return set_err(c, OM_ERR_INVALID, "width/height must be > 0");
     if ((uint64_t)p->width * p->height > (1ull << 31)) return set_err(c, OM_ERR_INVALID, "image too large");
     if (p->spp_total == 0) return set_err(c, OM_ERR_INVALID, "spp_total must be > 0");
     return OM_OK;

@@ -301,3 +301,42 @@ def test_concurrent_batches_are_bit_identical(om, oracle, streams):
     assert kt.launches[span] > 0 and kt.ms[span] > 0.0
     assert int(pix.pixels["n"].min()) == SPP and int(pix.pixels["n"].max()) == SPP
     assert L.lib.om_set_streams(fz.ctx, 5) == L.OM_ERR_INVALID
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
+@pytest.mark.parametrize("size", [(1, 1), (1, 7), (5, 1), (2, 2), (9, 3), (8, 8), (17, 9)])
+def test_degenerate_and_ragged_frames_bit_exact(om, oracle, pipeline, size):
+    """Frame edge cases: a 1-pixel-wide or -high frame divides by W-1 = 0 or H-1 = 0
+    (render_thread.rs:190-191), so its rays are non-finite and take the reference loop's
+    closed-form answer (hits.rs:274-285); partial 8x8 tiles; frames of exactly one tile."""
+    W, H = size
+    got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED), oracle.random_scene(0x5EED),
+                               om.default_camera(W / H), oracle.default_camera(W / H), W, H, 3, "auto",
+                               seed=21, pipeline=pipeline)
+    nb, msg = compare_stats(got, exp, f"{W}x{H}/{pipeline}")
+    assert nb == 0, msg
+    assert (got["n"] == 3).all()
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_sparse_worlds_bit_exact(om, oracle, pipeline):
+    """Worlds with a single primitive kind: one infinite plane (accepted by non-finite rays),
+    one sphere (the BVH2 holds a single leaf), and only marched objects (no traced list)."""
+    W, H, SPP = 24, 16, 3
+    cams = (om.default_camera(W / H), oracle.default_camera(W / H))
+    mats = (om.Material.new_lambertian((0.4, 0.5, 0.6)), oracle.material("lambertian", (0.4, 0.5, 0.6)))
+    builds = []
+    w, ow = om.HittableList.new(), oracle.World()
+    w += om.InfinitePlane.new((0., 0., 0.), (0., 1., 0.), mats[0]); ow.add_plane((0., 0., 0.), (0., 1., 0.), mats[1])
+    builds.append(("plane", w, ow))
+    w, ow = om.HittableList.new(), oracle.World()
+    w += om.Sphere.new_with_radius((0., 1., 0.), 1., mats[0]); ow.add_sphere_radius((0., 1., 0.), 1., mats[1])
+    builds.append(("sphere", w, ow))
+    w, ow = om.HittableList.new(), oracle.World()
+    w += om.MarchedSphere((0., 1., 0.), 1., mats[0]); ow.add_marched_sphere((0., 1., 0.), 1., mats[1])
+    builds.append(("marched", w, ow))
+    for name, w, ow in builds:
+        got, exp, _ = _render_both(om, oracle, w, ow, cams[0], cams[1], W, H, SPP, "auto", seed=22,
+                                   march_steps=256, pipeline=pipeline)
+        nb, msg = compare_stats(got, exp, f"{name}/{pipeline}")
+        assert nb == 0, msg
