@@ -355,7 +355,6 @@ om_status validate(om_ctx* c, const om_camera* cam, const om_render_params* p) {
     if (!c->have_world) return set_err(c, OM_ERR_STATE, "om_upload_world must precede rendering");
     if (p->width == 0 || p->height == 0) return set_err(c, OM_ERR_INVALID, "width/height must be > 0");
     if ((uint64_t)p->width * p->height > (1ull << 31)) return set_err(c, OM_ERR_INVALID, "image too large");
-    if (p->spp_total == 0) return set_err(c, OM_ERR_INVALID, "spp_total must be > 0");
     return OM_OK;
 }
 
@@ -405,6 +404,8 @@ om_status ensure_tile_lists(om_ctx* c, const om_camera* cam, uint32_t W, uint32_
 
 om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_pixel_stats* dev_stats,
                  const uint32_t* dev_pixels, uint32_t n_pixels, hipStream_t stream) {
+    // samples_per_pixel = 0: render()'s pass loop never runs (render_thread.rs:176), Stats untouched
+    if (p->spp_total == 0 || p->sample_count == 0) return OM_OK;
     om_status s = prepare_jitter(c, p->seed, p->spp_total);
     if (s) return s;
     if (!c->counters.p) {

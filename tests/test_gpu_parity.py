@@ -340,3 +340,20 @@ def test_sparse_worlds_bit_exact(om, oracle, pipeline):
                                    march_steps=256, pipeline=pipeline)
         nb, msg = compare_stats(got, exp, f"{name}/{pipeline}")
         assert nb == 0, msg
+
+
+def test_zero_samples_and_empty_frames(om):
+    """samples_per_pixel = 0 takes no sample (render()'s pass loop never runs) and leaves the
+    caller's Stats untouched; a 0-pixel frame is an argument error."""
+    from raytracingoneweekend_amd import _lib as L
+    W, H = 16, 8
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam)
+    pix = om.PixelsBox.new(W * H)
+    om.render(cam, fz, 50, 0.001, 100.0, 4, W, H, pix, seed=3, sample_count=2)
+    before = pix.pixels.copy()
+    om.render(cam, fz, 50, 0.001, 100.0, 0, W, H, pix, seed=3)
+    assert np.array_equal(before.view(np.uint8), pix.pixels.view(np.uint8))
+    with pytest.raises(L.OmError, match="width/height"):
+        om.render(cam, fz, 50, 0.001, 100.0, 4, 0, H, om.PixelsBox.new(0), seed=3)
