@@ -108,9 +108,10 @@ __host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
     return S.b2_lds_bytes ? 0u : (S.n_b2nodes < OM_WF_HYB_BYTES / 64u ? S.n_b2nodes : OM_WF_HYB_BYTES / 64u);
 }
 // Worlds with marched primitives: 1 (default) runs each bounce as a lane-refilling march
-// launch (k_march: every lane takes the segment's next path as soon as its march ends, so a
-// wave no longer waits for its longest march) followed by the shade+compact launch reading
-// the (closest, winner) it wrote; 0 keeps the fused trace+march+shade bounce kernel.
+// launch (k_march: lanes whose march ended take the segment's next paths together once
+// OM_WF_REFILL of them wait, so a wave no longer runs as long as its longest march) followed
+// by the shade+compact launch reading the (closest, winner) it wrote; 0 keeps the fused
+// trace+march+shade bounce kernel.
 #ifndef OM_WF_MARCH_SPLIT
 #define OM_WF_MARCH_SPLIT 1
 #endif
