@@ -71,7 +71,7 @@ FLOP_MARCH_STEP = 60      # one sphere-tracing iteration over the marched object
 BYTES_PER_LATER_SEGMENT = 128
 BYTES_PER_SAMPLE = 32
 BOUNCE_FAMILY = ("bounce0", "bounce", "tail")            # one fused trace+shade kernel body
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")          # C1; other configs: pmc_traffic_<config>.json
 
 
 def cpu_baseline(budget_s=12.0, cfg="C1"):
@@ -261,8 +261,9 @@ def main():
         nbytes = BYTES_PER_LATER_SEGMENT * (ctr.segments - ctr.samples) + BYTES_PER_SAMPLE * ctr.samples
         achieved_tflops = flops / span_s / 1e12
         traffic, traffic_src = None, None
-        if os.path.exists(PMC_TRAFFIC) and not mega and args.kernel == "auto" and args.config == "C1":
-            pm = json.load(open(PMC_TRAFFIC))
+        pmc_file = PMC_TRAFFIC if args.config == "C1" else PMC_TRAFFIC.replace(".json", f"_{args.config}.json")
+        if os.path.exists(pmc_file) and not mega and args.kernel == "auto":
+            pm = json.load(open(pmc_file))
             traffic, traffic_src = pm["hbm_bytes_per_launch"], pm["source"]
         roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": traffic,

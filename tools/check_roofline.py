@@ -9,7 +9,7 @@ import json
 import re
 import sys
 
-FAMILY = re.compile(r"k_(bounce0?|tail)<\d+, false")
+FAMILY = re.compile(r"k_(bounce|tail|march)<\d+, false|k_raygen<false>")   # bench.py's bounce family
 
 rows = [r for r in csv.DictReader(open(sys.argv[1])) if FAMILY.search(r["Name"])]
 calls = sum(int(r["Calls"]) for r in rows)

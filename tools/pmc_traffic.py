@@ -14,7 +14,7 @@ import os
 import re
 import sys
 
-FAMILY = re.compile(r"k_(bounce0?|tail)<\d+, false")
+FAMILY = re.compile(r"k_(bounce|tail|march)<\d+, false|k_raygen<false>")   # every bounce-family launch bench.py counts
 
 
 def per_launch(tag_dir, counter):
@@ -36,7 +36,8 @@ def main():
     write, nw = per_launch(tag, "WRITE_SIZE")
     if fetch is None or write is None:
         raise SystemExit("no FETCH_SIZE/WRITE_SIZE rows for the bounce kernels")
-    res = {"kernel": "k_bounce0+k_bounce+k_tail (fused trace+shade), production build",
+    res = {"kernel": "bounce family: k_bounce (bounce 0 and later) + k_tail, and k_raygen + k_march for marched "
+                     "worlds; production build",
            "hbm_bytes_per_launch": round(2.0 * fetch + write),
            "fetch_bytes_x2_per_launch": round(2.0 * fetch), "write_bytes_per_launch": round(write),
            "dispatches": {"FETCH_SIZE": nf, "WRITE_SIZE": nw},
