@@ -84,7 +84,7 @@ __host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
     return kBlk * ((TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) ? S.b4_stack : S.b2_stack) * 2u;
 }
 #ifndef OM_WF_TAIL_SPB
-#define OM_WF_TAIL_SPB 4
+#define OM_WF_TAIL_SPB 2
 #endif
 constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel

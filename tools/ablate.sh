@@ -22,7 +22,7 @@ declare -A V=(
   # cost split of the fused bounce kernel: run one half twice
   [trace2x]="$COMMON $DEV -DOM_ABLATE_TRACE2X"
   [tspb1]="$COMMON $DEV -DOM_WF_TAIL_SPB=1"
-  [tspb2]="$COMMON $DEV -DOM_WF_TAIL_SPB=2"
+  [tspb4]="$COMMON $DEV -DOM_WF_TAIL_SPB=4"
   [shade2x]="$COMMON $DEV -DOM_ABLATE_SHADE2X"
   [b512w6]="$COMMON $DEV -DOM_WF_BLOCK=512 -DOM_WF_WAVES=6"
   # bounce work distribution (bit-identical): block-step scan instead of per-wave LDS queues,
