@@ -42,6 +42,8 @@ declare -A V=(
   [msplit0]="$COMMON $DEV -DOM_WF_MARCH_SPLIT=0"
   [marrays]="$COMMON $DEV -DOM_MARCH_ARRAYS_ONLY"
   [mregs1]="$COMMON $DEV -DOM_WF_MARCH_REGS=1"
+  [refill12]="$COMMON $DEV -DOM_WF_REFILL=12"
+  [refill24]="$COMMON $DEV -DOM_WF_REFILL=24"
   [refill8]="$COMMON $DEV -DOM_WF_REFILL=8"
   [refill16]="$COMMON $DEV -DOM_WF_REFILL=16"
   [refill48]="$COMMON $DEV -DOM_WF_REFILL=48"
