@@ -1,6 +1,9 @@
 #!/bin/bash
 # Wavefront schedule sweep (C1, timing off).  Each argument after TAG is one case:
-#   "label|ENV=V ENV2=V|bench args"      e.g. "s2b2|OM_WF_STREAMS=2 OM_WF_BATCHES=2|--spp-per-step 32"
+#   "label|ENV=V ENV2=V|bench args"      e.g. "s2|ENV=1|--streams 2 --spp-per-step 32"
+# (The environment knobs of the r01_v6 schedule experiments, OM_WF_BATCHES / OM_WF_STAGGER,
+# lived only in experiment builds; the shipped schedule is set through bench.py's --streams,
+# --spp-per-step and --tail)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=$1; shift
