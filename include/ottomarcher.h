@@ -78,7 +78,10 @@ typedef struct om_pixel_stats {
 /* One render call = samples [sample_begin, sample_begin+sample_count) of every
  * (live) pixel, accumulated into the caller's om_pixel_stats in sample order.
  * spp_total sizes the jitter table (render_thread.rs:164-174); a pixel's sample
- * index is its Stats.n, exactly as jitters[pixel.stats.n] (render_thread.rs:188). */
+ * index is its Stats.n, exactly as jitters[pixel.stats.n] (render_thread.rs:188).
+ * As in the reference: spp_total or sample_count 0 takes no sample (the Stats are left
+ * as they are); width or height 1 divides by W-1 = 0 (render_thread.rs:190-191) and
+ * renders the resulting non-finite rays; width or height 0 is OM_ERR_INVALID. */
 typedef struct om_render_params {
     uint32_t width, height;     /* image_width / image_height */
     uint32_t spp_total;         /* samples_per_pixel of the whole frame */
