@@ -164,6 +164,10 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
                                               float nox, float noy, float noz, float t_lo, float& closest, int& best, Wk& w) {
     for (uint32_t k = 0; k < S.n_always2; ++k) {
         const OmAlwaysRec A = S.always2_rec[k];
+#ifndef OM_ALWAYS2_INF_SLAB
+        // an unbounded record (huge primitives, planes: lo = -inf) passes every slab test
+        if (A.lo[0] == -INFINITY) { offer(S, A.gi, o, d, tmin, closest, best, w); continue; }
+#endif
         w.add_pre();
         const float t_hi = closest * 1.0001f + 1e-3f;
         const float x0 = __builtin_fmaf(A.lo[0], ix, nox), x1 = __builtin_fmaf(A.hi[0], ix, nox);

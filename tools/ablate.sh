@@ -52,6 +52,8 @@ declare -A V=(
   [ab1]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=1"
   [ab4]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=4"
   [ab16]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=16"
+  # slab-test the unbounded always2 records too (the default skips their box)
+  [infslab]="$COMMON $DEV -DOM_ALWAYS2_INF_SLAB"
   [lpc2k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=2048"
   [lpc8k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=8192"
   [lpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=16384"
