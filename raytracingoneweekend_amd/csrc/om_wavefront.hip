@@ -135,6 +135,11 @@ __host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
 #ifndef OM_WF_ADAPTIVE_BATCH
 #define OM_WF_ADAPTIVE_BATCH 16
 #endif
+// k_bounce b >= 1: load the path's throughput/RNG/slot lanes before the trace (1: their latency hides
+// behind it, +1.3% on C1 over five A/B pairs) or after it (0).
+#ifndef OM_WF_EARLY_REST
+#define OM_WF_EARLY_REST 1
+#endif
 // Queue segments (= bounce workgroups) per CU: OM_WF_LANES_PER_CU / OM_WF_BLOCK.
 #ifndef OM_WF_LANES_PER_CU
 #define OM_WF_LANES_PER_CU 4096
@@ -414,6 +419,9 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
                 live = gen_path(P, R, i, p, p_pixel, res_id);
             } else {
                 load_ray(in, i, p);
+#if OM_WF_EARLY_REST
+                load_rest(in, i, p);       // issued before the trace: its latency hides behind it
+#endif
             }
             if (live) {
                 float closest;
@@ -443,7 +451,9 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
                     if (b2 != best || c2 != closest) res_id[0] = 0xDEADu;
                 }
 #endif
+#if !OM_WF_EARLY_REST
                 if (!FIRST) load_rest(in, i, p);
+#endif
 #ifdef OM_ABLATE_SHADE2X   // timing ablation: shade a copy first (same result slot, same values)
                 {
                     Path p2 = p;

@@ -54,6 +54,7 @@ declare -A V=(
   [ab16]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=16"
   # slab-test the unbounded always2 records too (the default skips their box)
   [infslab]="$COMMON $DEV -DOM_ALWAYS2_INF_SLAB"
+  [late]="$COMMON $DEV -DOM_WF_EARLY_REST=0"
   [lpc2k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=2048"
   [lpc8k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=8192"
   [lpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=16384"
