@@ -8,10 +8,18 @@ per-pixel Stats in HBM (render_thread.rs:176-199, batched).  16 steps of 32 spp 
 the full 512-spp frame; the library runs each step as two concurrent 16-spp batches
 (om_set_streams).
 
-N>1 (torch.distributed.run, one rank per GPU): 8x8 pixel tiles are dealt round-robin to
-ranks (main.rs:172-189's chunk round-robin); every rank renders its tiles at
-SPP_PER_STEP*N samples per step (fixed per-GPU work: weak scaling) and one RCCL gather
-of the finished f32 framebuffer to rank 0 closes the timed region.
+Every rank (N = 1 included) goes through the product's multi-GPU path: its
+8x8-tile shard of the frame (om_shard_pixels: main.rs:172-189's chunk round-robin, re-designed
+for GPUs) is rendered into an HBM-resident shard (om_render_shard), and the timed region ends
+with om_gather_frame, the RCCL grouped send/recv of every shard to rank 0 over xGMI plus the
+scatter into the W*H frame there.  N>1 (torch.distributed.run, one process per GPU): each rank
+renders its tiles at SPP_PER_STEP*N samples per step (fixed per-GPU work: weak scaling).
+torch.distributed (gloo, host memory) is the harness's control plane only: it hands RCCL's
+unique id from rank 0 to the others, and carries the barriers and the max-over-ranks time.
+
+At N=1 the line also carries `configs`: C2 (marched SDF scene, 256 march steps) and C3 (10k
+spheres, BVH) at full spp with their own roofline and CPU baseline, and C0 (the reference's
+CPU case, 400x225x64 at depth 8) timed on the GPU and on the host cores.
 
 Output: ONE JSON line on rank 0 (see DESIGN.md §7 for every field).
 """
@@ -19,6 +27,7 @@ import argparse
 import ctypes as C
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -33,17 +42,17 @@ import raytracingoneweekend_amd as om  # noqa: E402
 from raytracingoneweekend_amd import _lib as L  # noqa: E402
 from raytracingoneweekend_amd import shard  # noqa: E402
 
-W, H, MAX_DEPTH, TMIN, TMAX, SEED, SCENE_SEED = 1920, 1080, 50, 0.001, 100.0, 1, 0x5EED
+MAX_DEPTH, TMIN, TMAX, SEED, SCENE_SEED = 50, 0.001, 100.0, 1, 0x5EED
 SPP_PER_STEP = 32
-# BASELINE.json configs: C1 is the metric's workload (the default line); C2/C3/C4 are measured
-# with --config for DESIGN.md (the marched SDF scene at 256 march steps, the 10k-sphere BVH,
-# the 4K frame of the multi-GPU config).
+# BASELINE.json configs: C1 is the metric's workload (the default line); C2/C3 ride along in
+# the line's `configs` at N=1; C4 is the 4K frame of the multi-GPU config (--config C4).
 CONFIGS = {
+    "C0": {"scene": "S-traced", "spp": 64, "march_steps": 1024, "size": (400, 225), "depth": 8},
     "C1": {"scene": "S-traced", "spp": 512, "march_steps": 1024},
     "C2": {"scene": "S-marched", "spp": 256, "march_steps": 256},
     "C3": {"scene": "S-10k", "spp": 256, "march_steps": 1024},
-    # the multi-GPU config (BASELINE.json configs[4]: 3840x2160, 4096 spp, 8 GPUs); weak scaling
-    # as for C1: each rank renders its 1/N of the tiles at spp_per_step * N per step
+    # BASELINE.json configs[4]: 3840x2160, 4096 spp, 8 GPUs; each rank renders its 1/N of the
+    # tiles at 4096 spp: the fixed frame (strong scaling)
     "C4": {"scene": "S-traced", "spp": 4096, "march_steps": 1024, "size": (3840, 2160)},
 }
 
@@ -54,6 +63,8 @@ def make_scene(name, om_or_oracle):
     if name == "S-marched":
         return om_or_oracle.marched_scene()
     return om_or_oracle.random_scene(SCENE_SEED, grid_half=50, extras=False)
+
+
 PEAK_TFLOPS = 157.3   # MI355X FP32 vector peak (MI355X_MICROARCH.md; FMA = 2 flop)
 ISSUE_PEAK_TFLOPS = 78.6  # one f32 op per lane per cycle: 256 CU x 4 SIMD-32 x 32 lanes x 2.4 GHz (no FMA)
 PEAK_HBM_GBS = 8000.0
@@ -65,90 +76,75 @@ FLOP_BOX_TEST = 25        # slab test of one BVH child box
 FLOP_SEGMENT = 110        # finalize (point + normal) + scatter + throughput + loop bookkeeping
 FLOP_CAMERA_RAY = 50      # jitter/uv + lens disc + get_ray (bounce 0, once per sample)
 FLOP_MARCH_STEP = 60      # one sphere-tracing iteration over the marched objects (S-traced: none)
-# Algorithmic HBM bytes of the bounce kernels (SoA path queue): a segment
-# after the first reads its 64-B path and writes the 64-B survivor; a sample reads its
-# pixel id + Stats.n/flags (12 B) and writes its result (20 B).
+# Algorithmic HBM bytes of the bounce-family kernels (SoA path queues).
+# Fused pipeline (traced worlds): a segment after the first reads its 64-B path and the
+# previous bounce wrote it (128 B); a sample reads its pixel id + Stats.n/flags (12 B) and
+# writes its result (20 B).  Split march pipeline (marched worlds, §5.8): k_raygen writes every
+# sample's 64-B camera path, so every segment is written and read once (128 B), k_march reads
+# its origin + direction (32 B) and writes an 8-B hit record that k_bounce<HIT> reads (16 B).
 BYTES_PER_LATER_SEGMENT = 128
 BYTES_PER_SAMPLE = 32
-BOUNCE_FAMILY = ("bounce0", "bounce", "tail")            # one fused trace+shade kernel body
+BYTES_PER_SEGMENT_SPLIT = 128 + 32 + 16
+BOUNCE_FAMILY = ("bounce0", "bounce", "tail")            # trace+shade launches (+ k_raygen/k_march: split)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")          # C1; other configs: pmc_traffic_<config>.json
 
 
-def cpu_baseline(budget_s=12.0, cfg="C1"):
-    """Oracle (CPU restatement, `port`) on the host: the reference's thread scheme
-    (num_cpus-1 workers, 2730-px round-robin chunks, main.rs:170-189) on the same frame."""
-    from oracle import oracle as O  # checker / baseline only
-    cores = max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 2)) - 1)
-    ow = make_scene(CONFIGS[cfg]["scene"], O)
-    # the oracle is brute force: for the 10k-sphere scene a 1/64-area frame of the same
-    # scene and camera (per-sample cost does not depend on the resolution)
-    w, h = (W // 8, H // 8) if cfg == "C3" else (W, H)
-    cam = O.default_camera(w / h)
-    done, t_total, passes = 0, 0.0, 0
-    stats = np.zeros(w * h, dtype=O.PIXEL_STATS_DTYPE)
-    spp_total = 64
-    while passes == 0 or (t_total < budget_s and passes < spp_total):
-        p = O.params(w, h, spp_total, sample_count=1, max_depth=MAX_DEPTH, seed=SEED,
-                     march_steps=CONFIGS[cfg]["march_steps"])
-        t0 = time.perf_counter()
-        _, ctr = O.render(ow, cam, p, stats=stats, nthreads=cores)
-        t_total += time.perf_counter() - t0
-        done += ctr["samples"]
-        passes += 1
-    return {"value": done / t_total / 1e6, "unit": "Msamples/s", "cores": cores, "kind": "port",
-            "sample": f"{cfg} frame {w}x{h}, {passes} spp (full passes), depth {MAX_DEPTH}, {CONFIGS[cfg]['scene']}, "
-                      f"{cores} threads, {t_total:.1f} s"}
+def cpu_baseline(cfg, budget_s, lib="liboro.so"):
+    """The oracle (CPU restatement, `port`) on the host cores, in a child process
+    (oracle/cpu_bench.py, which never touches the GPU): the reference's thread scheme on the
+    config's frame for about `budget_s` seconds of full 1-spp passes.  `lib` picks the build
+    (liboro.so: -O3 default x86-64; liboro_v3.so: -O3 -march=x86-64-v3)."""
+    env = dict(os.environ, ORO_LIB=lib)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_bench.py"), "--config", cfg,
+                        "--budget", str(budget_s)], env=env, capture_output=True, text=True, timeout=600)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu baseline {cfg}/{lib} failed: {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--config", default="C1", choices=list(CONFIGS))
-    ap.add_argument("--steps", type=int, default=None, help="default: the config's spp / spp-per-step (C1: 32)")
-    ap.add_argument("--spp-per-step", type=int, default=SPP_PER_STEP, help="samples per pixel per step (one render call)")
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
-    ap.add_argument("--pipeline", default="auto", choices=list(L.PIPELINES))
-    ap.add_argument("--tail", type=int, default=0, help="first bounce of the persistent tail launch (0 = library default)")
-    ap.add_argument("--streams", type=int, default=2, help="wavefront batches in flight per call (om_set_streams; 1 = serial)")
-    ap.add_argument("--kernel-timing", default="span", choices=["span", "launch", "off"],
-                    help="HIP events in the timed region: span = once around each batch's bounce kernels "
-                         "(2 events/step, default), launch = around every launch (per-kernel breakdown)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl (= RCCL over xGMI, the measured path); gloo gathers through host memory and maps "
-                         "ranks onto the visible GPUs (a functional rehearsal of N>1 on a 1-GPU box)")
-    ap.add_argument("--primary-lists", default="auto", choices=["off", "auto", "on"],
-                    help="bounce-0 per-tile candidate lists (DESIGN.md §5.10); auto = when they average <= 12")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-budget", type=float, default=12.0)
-    args = ap.parse_args()
-    cfg = CONFIGS[args.config]
-    global W, H
-    W, H = cfg.get("size", (W, H))
-    if args.steps is None:
-        args.steps = cfg["spp"] // (args.spp_per_step * args.gpus) if args.config == "C4" else cfg["spp"] // args.spp_per_step
+class Control:
+    """Harness control plane (gloo over host memory; absent at N=1): RCCL id hand-off,
+    barriers, max over ranks.  No frame data goes through it."""
 
-    world_size = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world_size != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
-    gloo = args.dist_backend == "gloo"
-    if gloo:
-        local_rank = local_rank % max(1, torch.cuda.device_count())
-    torch.cuda.set_device(local_rank)
-    if world_size > 1:
-        if gloo:
+    def __init__(self, world_size, rank):
+        self.n, self.rank = world_size, rank
+        if world_size > 1:
             dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
-    # ---- setup (not timed): scene build + freeze/upload, camera, tile lists
-    # a dedicated (non-NULL) stream: the kernel, its HIP events and the collectives all run on it
+    def unique_id(self):
+        uid = [shard.unique_id() if self.rank == 0 else None]
+        if self.n > 1:
+            dist.broadcast_object_list(uid, src=0)
+        return uid[0]
+
+    def barrier(self):
+        if self.n > 1:
+            dist.barrier()
+
+    def max(self, x):
+        if self.n == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        if self.n > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+
+
+def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_mode, pmc_ok=True):
+    """One config through the product path; returns the measured fields (value, roofline, work)."""
+    cfg = CONFIGS[name]
+    W, H = cfg.get("size", (1920, 1080))
+    depth = cfg.get("depth", MAX_DEPTH)
+    n, rank = ctl.n, ctl.rank
+    # a dedicated (non-NULL) stream: the kernels, their HIP events and the RCCL gather run on it
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
-    sptr = C.c_void_p(stream.cuda_stream)
-    assert sptr.value, "need a non-default stream handle"
+    sptr = stream.cuda_stream
+    assert sptr, "need a non-default stream handle"
     world = make_scene(cfg["scene"], om)
     cam = om.default_camera(W / H)
     frozen = world.freeze(cam, device=local_rank, kernel=args.kernel, pipeline=args.pipeline)
@@ -156,100 +152,94 @@ def main():
     L.check(L.lib.om_set_tail_bounce(ctx, args.tail), ctx)
     L.check(L.lib.om_set_streams(ctx, args.streams), ctx)
     L.check(L.lib.om_set_primary_lists(ctx, {"off": 0, "auto": 1, "on": 2}[args.primary_lists]), ctx)
-    spp_step = args.spp_per_step * world_size                # fixed per-GPU samples per step
-    spp_total = spp_step * args.steps
-    pix = shard.tile_pixels(W, H, rank, world_size)
-    n_px = int(pix.size)
-    dev_pix = torch.from_numpy(pix.view(np.int32)).cuda()
-    stats = torch.zeros(n_px * 40, dtype=torch.uint8, device="cuda")
-
-    def step(p):
-        L.check(L.lib.om_render_device_pixels(ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(stats.data_ptr()),
-                                              C.c_void_p(dev_pix.data_ptr()), n_px, sptr), ctx)
-
-    p = om.make_params(MAX_DEPTH, TMIN, TMAX, spp_total, W, H, sample_count=spp_step, seed=SEED,
+    comm = shard.Comm(ctx, n, rank, ctl.unique_id())
+    spp_step = spp_per_step * (1 if name == "C4" else n)          # C4: fixed frame; else fixed per-GPU work
+    spp_total = spp_step * steps
+    cap = shard.shard_capacity(W, H, n)
+    n_mine = shard.tile_pixels(W, H, rank, n).size
+    sh = torch.zeros(cap * 40, dtype=torch.uint8, device="cuda")
+    frame = torch.zeros((W * H if rank == 0 else 1) * 40, dtype=torch.uint8, device="cuda")
+    p = om.make_params(depth, TMIN, TMAX, spp_total, W, H, sample_count=spp_step, seed=SEED,
                        march_steps=cfg["march_steps"])
-    for _ in range(args.warmup):
-        step(p)
-    torch.cuda.synchronize()
-    stats.zero_()                                            # timed frame starts from empty Stats
-    L.check(L.lib.om_set_counting(ctx, 0), ctx)              # production build: counters compiled out
-    for _ in range(args.warmup):                             # warm the non-counting kernel too
-        step(p)
-    torch.cuda.synchronize()
-    stats.zero_()
-    gathered, send = None, None
-    if world_size > 1:                                       # gather buffers (equal-size shards), allocated untimed
-        n_max = shard.shard_capacity(W, H, world_size) * 40
-        send = torch.zeros(n_max, dtype=torch.uint8, device="cpu" if gloo else "cuda")
-        gathered = [torch.empty_like(send) for _ in range(world_size)] if rank == 0 else None
+
+    def step():
+        comm.render_shard(cam, p, sh.data_ptr(), sptr)
+
+    for count in (1, 0):                                      # warm the counting and the production build
+        L.check(L.lib.om_set_counting(ctx, count), ctx)
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize()
+        sh.zero_()
     torch.cuda.synchronize()
 
     kt = L.om_kernel_times()
-    timing = args.kernel_timing != "off"
-    L.check(L.lib.om_set_timing(ctx, {"off": 0, "launch": 1, "span": 2}[args.kernel_timing]), ctx)   # events on `stream`
+    timing = timing_mode != "off"
+    L.check(L.lib.om_set_timing(ctx, {"off": 0, "launch": 1, "span": 2}[timing_mode]), ctx)   # events on `stream`
 
     # ---- timed region
-    if world_size > 1:
-        dist.barrier()
+    ctl.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(p)
-    if world_size > 1:                                       # RCCL gather of the f32 framebuffer to rank 0
-        send[: stats.numel()] = stats.cpu() if gloo else stats
-        dist.gather(send, gathered, dst=0)
+    for _ in range(steps):
+        step()
+    comm.gather_frame(sh.data_ptr(), W, H, frame.data_ptr(), sptr)   # RCCL: every shard to rank 0
     torch.cuda.synchronize()
-    if world_size > 1:
-        dist.barrier()
+    ctl.barrier()
     elapsed = time.perf_counter() - t0
     # ---- end timed region
 
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if gloo else "cuda")
-    if world_size > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = ctl.max(elapsed)
     L.check(L.lib.om_get_kernel_times(ctx, C.byref(kt)), ctx)
     L.check(L.lib.om_set_timing(ctx, 0), ctx)
-    host = stats.cpu().numpy().view(L.PIXEL_STATS_DTYPE).copy()
-    assert int(host["n"].min()) == spp_total and int(host["n"].max()) == spp_total, "every pixel must take every sample"
+    host = sh.cpu().numpy().copy()
+    mine = host[: n_mine * 40].view(L.PIXEL_STATS_DTYPE)
+    assert int(mine["n"].min()) == spp_total and int(mine["n"].max()) == spp_total, "every pixel must take every sample"
+    if rank == 0:
+        fr = frame.cpu().numpy().view(L.PIXEL_STATS_DTYPE)
+        assert int(fr["n"].min()) == spp_total and int(fr["n"].max()) == spp_total, "gathered frame incomplete"
+        assert np.array_equal(fr[shard.tile_pixels(W, H, 0, n)].view(np.uint8).reshape(-1), host[: n_mine * 40]), \
+            "gathered frame differs from rank 0's shard"
 
     # per-launch durations (untimed): the same K steps again, production build, every launch
     # bracketed by events on its stream (om_set_timing 1) -> the rocprof-comparable average
-    # launch duration and the launch concurrency inside a call; same frame, bit for bit
+    # launch duration and the launch concurrency inside a call; same shard, bit for bit
     mega = kt.launches[L.KT_CLASSES.index("megakernel")] > 0     # the pipeline that actually ran (auto)
     fam = [L.KT_CLASSES.index("megakernel")] if mega else [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
     span_i = L.KT_CLASSES.index("megakernel" if mega else "bounce_span")
     kl = L.om_kernel_times()
     if timing:
-        stats.zero_()
+        sh.zero_()
         L.check(L.lib.om_set_timing(ctx, 1), ctx)
-        for _ in range(args.steps):
-            step(p)
+        for _ in range(steps):
+            step()
         torch.cuda.synchronize()
         L.check(L.lib.om_get_kernel_times(ctx, C.byref(kl)), ctx)
         L.check(L.lib.om_set_timing(ctx, 0), ctx)
-        assert np.array_equal(stats.cpu().numpy(), host.view(np.uint8)), "per-launch timing changed the result"
+        assert np.array_equal(sh.cpu().numpy(), host), "per-launch timing changed the result"
 
-    # work counting (untimed): the same K steps again with the counting build; the
-    # frame it produces must equal the timed one bit for bit (counters change nothing)
-    stats.zero_()
-    L.check(L.lib.om_reset_counters(ctx, sptr), ctx)
+    # work counting (untimed): the same K steps again with the counting build; the shard it
+    # produces must equal the timed one bit for bit (counters change nothing)
+    sh.zero_()
+    L.check(L.lib.om_reset_counters(ctx, C.c_void_p(sptr)), ctx)
     L.check(L.lib.om_set_counting(ctx, 1), ctx)
-    for _ in range(args.steps):
-        step(p)
+    for _ in range(steps):
+        step()
     torch.cuda.synchronize()
     ctr = L.om_counters()
     L.check(L.lib.om_get_counters(ctx, C.byref(ctr)), ctx)
-    assert np.array_equal(stats.cpu().numpy(), host.view(np.uint8)), "counting build changed the result"
+    assert np.array_equal(sh.cpu().numpy(), host), "counting build changed the result"
+    comm.close()
+    frozen.close()
 
-    total_samples = W * H * spp_total                          # all ranks together
+    total_samples = W * H * spp_total        # all ranks together (each renders its 1/N of the pixels)
     value = total_samples / elapsed / 1e6
+    marched = cfg["scene"] == "S-marched"
 
-    # roofline of the dominant kernel: the fused trace+shade bounce kernel (all its launches:
-    # bounce 0, bounces 1.., tail), algorithmic flops from the live counters.  Its launches run
-    # two at a time (concurrent batches), so the rate is the family's flops over the time it
-    # holds the GPU: the timed region's call spans (events on the call's stream).
+    # roofline of the dominant kernel: the trace+shade bounce family (all its launches: bounce 0,
+    # bounces 1.., tail; marched worlds also k_raygen and k_march), algorithmic flops from the
+    # live counters.  Its launches run two at a time (concurrent batches), so the rate is the
+    # family's flops over the time it holds the GPU: the timed region's call spans.
     launches = sum(kl.launches[i] for i in fam) if timing else 0
     roof = None
     if timing and launches:
@@ -258,68 +248,164 @@ def main():
         rerun_span_s = kl.ms[span_i] / 1e3
         flops = (FLOP_EXACT_TEST * ctr.prim_tests + FLOP_BOX_TEST * ctr.pre_tests + FLOP_SEGMENT * ctr.segments
                  + FLOP_CAMERA_RAY * ctr.samples + FLOP_MARCH_STEP * ctr.march_steps)
-        nbytes = BYTES_PER_LATER_SEGMENT * (ctr.segments - ctr.samples) + BYTES_PER_SAMPLE * ctr.samples
+        if marched and not mega:
+            nbytes = BYTES_PER_SEGMENT_SPLIT * ctr.segments + BYTES_PER_SAMPLE * ctr.samples
+        else:
+            nbytes = BYTES_PER_LATER_SEGMENT * (ctr.segments - ctr.samples) + BYTES_PER_SAMPLE * ctr.samples
         achieved_tflops = flops / span_s / 1e12
         traffic, traffic_src = None, None
-        pmc_file = PMC_TRAFFIC if args.config == "C1" else PMC_TRAFFIC.replace(".json", f"_{args.config}.json")
-        if os.path.exists(pmc_file) and not mega and args.kernel == "auto":
+        pmc_file = PMC_TRAFFIC if name == "C1" else PMC_TRAFFIC.replace(".json", f"_{name}.json")
+        if pmc_ok and os.path.exists(pmc_file) and not mega and args.kernel == "auto":
             pm = json.load(open(pmc_file))
             traffic, traffic_src = pm["hbm_bytes_per_launch"], pm["source"]
         roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": traffic,
                 "issue_peak": ISSUE_PEAK_TFLOPS, "frac_of_issue_peak": round(achieved_tflops / ISSUE_PEAK_TFLOPS, 4),
-                "kernel": "render_kernel (megakernel)" if mega else "k_bounce0+k_bounce+k_tail (fused trace+shade)",
-                "launches_per_step": round(launches / args.steps, 2),
+                "kernel": "render_kernel (megakernel)" if mega else
+                          ("k_raygen+k_march+k_bounce<HIT>+k_tail (split march)" if marched else
+                           "k_bounce0+k_bounce+k_tail (fused trace+shade)"),
+                "launches_per_step": round(launches / steps, 2),
                 "avg_launch_ms": round(per_launch_s * 1e3, 4),
                 "effective_ms_per_launch": round(span_s / launches * 1e3, 4),
                 "launch_concurrency": round(per_launch_s * launches / rerun_span_s, 3) if rerun_span_s else None,
                 "flop_per_launch": round(flops / launches), "algorithmic_bytes_per_launch": round(nbytes / launches),
                 "hbm_achieved_gbs": round(nbytes / span_s / 1e9, 2), "traffic_source": traffic_src,
-                "kernel_share_of_step": round(span_s / elapsed, 4), "timing": args.kernel_timing,
-                "all_kernels_ms_per_step": {k: round(kl.ms[i] / args.steps, 4) for i, k in enumerate(L.KT_CLASSES)
+                "traffic_over_algorithmic": round(traffic / (nbytes / launches), 3) if traffic else None,
+                "kernel_share_of_step": round(span_s / elapsed, 4), "timing": timing_mode,
+                "all_kernels_ms_per_step": {k: round(kl.ms[i] / steps, 4) for i, k in enumerate(L.KT_CLASSES)
                                             if kl.launches[i]}}
-    hbm_gbs = roof["hbm_achieved_gbs"] if roof else None
+    return {
+        "value": round(value, 3), "elapsed_s": elapsed, "steps": steps, "W": W, "H": H, "depth": depth,
+        "spp_total": spp_total, "spp_step": spp_step, "mega": mega, "roofline": roof,
+        "work": {"segments_per_sample": round(ctr.segments / max(1, ctr.samples), 4),
+                 "prim_tests_per_segment": round(ctr.prim_tests / max(1, ctr.segments), 3),
+                 "box_tests_per_segment": round(ctr.pre_tests / max(1, ctr.segments), 3),
+                 "march_steps_per_segment": round(ctr.march_steps / max(1, ctr.segments), 3),
+                 "gsegments_per_s": round(ctr.segments * n / elapsed / 1e9, 4)},
+    }
+
+
+def workload(name, r):
+    cfg = CONFIGS[name]
+    return (f"{name} {cfg['scene']} {r['W']}x{r['H']}, {r['spp_total']} spp timed ({r['spp_step']} spp/step), "
+            f"depth {r['depth']}" + (f", {cfg['march_steps']} march steps" if name == "C2" else ""))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="C1", choices=[c for c in CONFIGS if c != "C0"])
+    ap.add_argument("--steps", type=int, default=None, help="default: the config's spp / spp-per-step (C1: 16)")
+    ap.add_argument("--spp-per-step", type=int, default=SPP_PER_STEP, help="samples per pixel per step (one render call)")
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
+    ap.add_argument("--pipeline", default="auto", choices=list(L.PIPELINES))
+    ap.add_argument("--tail", type=int, default=0, help="first bounce of the persistent tail launch (0 = library default)")
+    ap.add_argument("--streams", type=int, default=2, help="wavefront batches in flight per call (om_set_streams; 1 = serial)")
+    ap.add_argument("--kernel-timing", default="span", choices=["span", "launch", "off"],
+                    help="HIP events in the timed region: span = once around each call's bounce kernels "
+                         "(2 events/step, default), launch = around every launch (per-kernel breakdown)")
+    ap.add_argument("--primary-lists", default="auto", choices=["off", "auto", "on"],
+                    help="bounce-0 per-tile candidate lists (DESIGN.md §5.10); auto = when they average <= 12")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="quick mode: the headline config only (no CPU baselines, no `configs` block)")
+    ap.add_argument("--no-extras", action="store_true", help="no `configs` block (C2/C3/C0) at N=1")
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world_size != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
+    torch.cuda.set_device(local_rank)
+    ctl = Control(world_size, rank)
+    steps = args.steps
+    if steps is None:
+        steps = cfg["spp"] // args.spp_per_step if args.config != "C4" else cfg["spp"] // args.spp_per_step
+    r = run_config(args.config, args, ctl, local_rank, steps, args.warmup, args.spp_per_step, args.kernel_timing)
+
+    extras = None
+    quick = args.no_cpu_baseline or args.no_extras
+    if rank == 0 and world_size == 1 and not quick and args.config == "C1":
+        extras = {}
+        for name in ("C2", "C3"):
+            c = CONFIGS[name]
+            e = run_config(name, args, ctl, local_rank, c["spp"] // args.spp_per_step, 1, args.spp_per_step, "span")
+            extras[name] = {"metric": "Msamples/s", "value": e["value"], "ms_per_step": round(e["elapsed_s"] / e["steps"] * 1e3, 4),
+                            "workload": workload(name, e), "pipeline": "megakernel" if e["mega"] else "wavefront",
+                            "roofline": e["roofline"], "work": e["work"],
+                            "cpu_baseline": cpu_baseline(name, min(8.0, args.cpu_budget))}
+        extras["C0"] = run_c0(args)
+    cpu = None
+    if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.config, args.cpu_budget)
+        cpu["second"] = cpu_baseline(args.config, args.cpu_budget, "liboro_v3.so")
 
     if rank == 0:
-        if gathered is not None:                             # assemble + verify the gathered frame (untimed)
-            frame = shard.assemble(W, H, [g.cpu().numpy() for g in gathered])
-            assert int(frame["n"].min()) == spp_total, "gathered frame incomplete"
-        cpu = None
-        if world_size == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.cpu_budget, args.config)
         out = {
             "metric": "Msamples/s (W×H×spp/s) + achieved HBM GB/s, 1080p@512spp traced scene",
-            "value": round(value, 3),
+            "value": r["value"],
             "unit": "Msamples/s",
             "n_gpus": world_size,
-            "steps": args.steps,
+            "steps": steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(r["elapsed_s"] / steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "strong" if args.config == "C4" else "weak",   # C4: the fixed 4K x 4096-spp frame
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic: {cfg['scene']} (om-rng scene seed 0x5EED), render seed 1",
-            "config": {"workload": f"{args.config} {cfg['scene']} {W}x{H}, {spp_total} spp timed ({spp_step} spp/step), "
-                                   f"depth {MAX_DEPTH}" + (f", {cfg['march_steps']} march steps" if args.config == "C2" else ""),
-                       "width": W, "height": H, "spp_per_step": spp_step, "max_depth": MAX_DEPTH,
-                       "parallelism": f"tile{world_size}" + ("/gloo" if gloo and world_size > 1 else ""),
+            "config": {"workload": workload(args.config, r), "width": r["W"], "height": r["H"],
+                       "spp_per_step": r["spp_step"], "max_depth": r["depth"],
+                       "parallelism": f"tile{world_size}", "gather": "RCCL send/recv (om_gather_frame)",
                        "kernel": args.kernel,
-                       "pipeline": args.pipeline + (("->megakernel" if mega else "->wavefront") if args.pipeline == "auto" else ""),
+                       "pipeline": args.pipeline + (("->megakernel" if r["mega"] else "->wavefront")
+                                                    if args.pipeline == "auto" else ""),
                        "tail_bounce": args.tail or "default", "streams": args.streams},
-            "hbm_gbs": hbm_gbs,
-            "roofline": roof,
-            "work": {"segments_per_sample": round(ctr.segments / max(1, ctr.samples), 4),
-                     "prim_tests_per_segment": round(ctr.prim_tests / max(1, ctr.segments), 3),
-                     "box_tests_per_segment": round(ctr.pre_tests / max(1, ctr.segments), 3),
-                     "march_steps_per_segment": round(ctr.march_steps / max(1, ctr.segments), 3),
-                     "gsegments_per_s": round(ctr.segments * world_size / elapsed / 1e9, 4)},
+            "hbm_gbs": r["roofline"]["hbm_achieved_gbs"] if r["roofline"] else None,
+            "roofline": r["roofline"],
+            "work": r["work"],
             "cpu_baseline": cpu,
+            "configs": extras,
         }
         print(json.dumps(out))
-    if world_size > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    ctl.close()
+
+
+def run_c0(args, reps=20):
+    """C0, the reference's CPU case (BASELINE.json configs[0]: 400x225, 64 spp, depth 8): the
+    whole 64-spp frame per step on the GPU (device-resident Stats, zeroed before each frame)
+    beside the CPU oracle rendering the same frame (the frame tests/test_golden.py and the
+    parity tests hold bit-identical between the two)."""
+    cfg = CONFIGS["C0"]
+    W, H = cfg["size"]
+    world = make_scene(cfg["scene"], om)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam)
+    L.check(L.lib.om_set_counting(fz.ctx, 0), fz.ctx)
+    stream = torch.cuda.Stream()
+    frames = [torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda") for _ in range(reps + 1)]
+    p = om.make_params(cfg["depth"], TMIN, TMAX, cfg["spp"], W, H, seed=SEED)
+
+    def frame(buf):
+        L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(buf.data_ptr()),
+                                       C.c_void_p(stream.cuda_stream)), fz.ctx)
+    frame(frames[-1])                                                      # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in frames[:reps]:
+        frame(b)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / reps
+    got = frames[0].cpu().numpy()
+    fz.close()
+    cpu = cpu_baseline("C0", 0.0)
+    return {"metric": "Msamples/s", "value": round(W * H * cfg["spp"] / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 4),
+            "workload": f"C0 S-traced {W}x{H}, {cfg['spp']} spp, depth {cfg['depth']} (whole frame per step, {reps} frames)",
+            "frame_n_ok": bool((got.view(L.PIXEL_STATS_DTYPE)["n"] == cfg["spp"]).all()),
+            "cpu_baseline": cpu, "gpu_over_cpu": round(W * H * cfg["spp"] / dt / 1e6 / cpu["value"], 1)}
 
 
 if __name__ == "__main__":

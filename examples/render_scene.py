@@ -1,7 +1,7 @@
 """Headless counterpart of the reference front-end (main.rs:123-214 + draw_to_sdl):
 compose random_scene through the Camera/Material/HittableList API, render it
 progressively on the GPU like the reference's render threads (adaptive retirement
-optional), then save every display view (keys 0-6 of main.rs:360-367) as BMP/PPM —
+by default, --fixed-spp to take every sample), then save every display view (keys 0-6 of main.rs:360-367) as BMP/PPM —
 the F12 save of main.rs:473-476.
 
     python examples/render_scene.py --width 1000 --height 666 --spp 200 --out out/
@@ -25,7 +25,9 @@ def main():
     ap.add_argument("--spp", type=int, default=200)              # main.rs:145
     ap.add_argument("--max-depth", type=int, default=50)         # main.rs:146
     ap.add_argument("--per-call", type=int, default=8, help="samples per render call (progressive passes)")
-    ap.add_argument("--adaptive", action="store_true", help="retire converged pixels (render_thread.rs:31-38)")
+    ap.add_argument("--fixed-spp", dest="adaptive", action="store_false",
+                    help="take every sample of every pixel (default: retire converged pixels like the "
+                         "reference's render threads, render_thread.rs:31-38,97-101)")
     ap.add_argument("--torus", action="store_true", help="include the marched torus block of main.rs:73-81")
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--out", default="out")

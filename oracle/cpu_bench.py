@@ -1,0 +1,78 @@
+"""CPU baseline timing of the oracle (bench.py's `cpu_baseline` leg; test infrastructure, never
+the product).  Runs the reference's thread scheme (num_cpus-1 workers over 2730-pixel
+round-robin chunks, main.rs:170-189) over full 1-spp passes of a config's frame until a time
+budget is spent, and prints one JSON object.  Which build is timed is chosen by ORO_LIB
+(liboro.so: -O3, default x86-64 target; liboro_v3.so: -O3 -march=x86-64-v3), so bench.py runs
+this as a subprocess once per build.
+
+    ORO_LIB=liboro_v3.so python oracle/cpu_bench.py --config C1 --budget 12 --threads 15
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path[0] = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # the repo root, not oracle/
+from oracle import oracle as O  # noqa: E402
+
+SCENES = {"C0": "S-traced", "C1": "S-traced", "C2": "S-marched", "C3": "S-10k", "C4": "S-traced"}
+MARCH = {"C2": 256}
+FRAMES = {"C0": (400, 225), "C1": (1920, 1080), "C2": (1920, 1080), "C3": (240, 135), "C4": (1920, 1080)}
+DEPTH = {"C0": 8}
+
+
+def scene(cfg):
+    s = SCENES[cfg]
+    if s == "S-traced":
+        return O.random_scene(0x5EED)
+    if s == "S-marched":
+        return O.marched_scene()
+    return O.random_scene(0x5EED, grid_half=50, extras=False)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def run(cfg, budget_s, threads, spp_total=64, seed=1):
+    """Full 1-spp passes of the config's frame (C3: a 1/64-area frame of the same scene and camera,
+    since the oracle is brute force over 10k spheres and the per-sample cost does not depend on
+    the resolution; C0: its whole 400x225x64 frame at depth 8)."""
+    w, h = FRAMES[cfg]
+    depth = DEPTH.get(cfg, 50)
+    ow, cam = scene(cfg), O.default_camera(w / h)
+    stats = np.zeros(w * h, dtype=O.PIXEL_STATS_DTYPE)
+    done, t_total, passes = 0, 0.0, 0
+    full = cfg == "C0"                                         # the CPU config: the whole frame
+    while passes == 0 or (passes < spp_total and (full or t_total < budget_s)):
+        p = O.params(w, h, spp_total, sample_count=1, max_depth=depth, seed=seed,
+                     march_steps=MARCH.get(cfg, 1024))
+        t0 = time.perf_counter()
+        _, ctr = O.render(ow, cam, p, stats=stats, nthreads=threads)
+        t_total += time.perf_counter() - t0
+        done += ctr["samples"]
+        passes += 1
+    return {"value": done / t_total / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "build": os.path.basename(O.LIB), "seconds": round(t_total, 3), "samples": int(done),
+            "nproc": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"{cfg} frame {w}x{h}, {passes} spp (full 1-spp passes), depth {depth}, {SCENES[cfg]}, "
+                      f"{threads} threads ({os.path.basename(O.LIB)}), {t_total:.1f} s"}
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C1", choices=list(SCENES))
+    ap.add_argument("--budget", type=float, default=12.0)
+    ap.add_argument("--threads", type=int, default=0, help="0: num_cpus-1 as main.rs:170 (OMP_NUM_THREADS-1 if set)")
+    a = ap.parse_args()
+    t = a.threads or max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 2)) - 1)
+    print(json.dumps(run(a.config, a.budget, t)))

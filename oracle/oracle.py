@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB = os.path.join(HERE, "liboro.so")
+# ORO_LIB: another build of the same restatement (liboro_v3.so: the x86-64-v3 CPU baseline)
+LIB = os.path.join(HERE, os.environ.get("ORO_LIB", "liboro.so"))
 
 PIXEL_STATS_DTYPE = np.dtype([("bloom", "<u8"), ("sum", "<f4", (3,)), ("n", "<u4"), ("avg_depth", "<f4"),
                               ("bad_avgs", "<u4"), ("color", "u1", (3,)), ("flags", "u1"), ("reserved", "<u4")])
@@ -37,7 +38,7 @@ def build():
     """Compile liboro.so (gcc, -ffp-contract=off) if it is missing or stale."""
     src = os.path.join(HERE, "om_oracle.cpp")
     if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(src):
-        subprocess.check_call(["make", "-C", HERE, "liboro.so"], stdout=subprocess.DEVNULL)
+        subprocess.check_call(["make", "-C", HERE, os.path.basename(LIB)], stdout=subprocess.DEVNULL)
 
 
 def _load():

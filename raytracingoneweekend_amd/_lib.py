@@ -62,7 +62,7 @@ assert PIXEL_STATS_DTYPE.itemsize == 40
 
 # every symbol include/ottomarcher.h declares (tests check the library exports all of them)
 EXPORTS = [
-    "om_abi_version", "om_material_lambertian", "om_material_metal", "om_material_metal_fuzz", "om_material_dielectric",
+    "om_abi_version", "om_build_id", "om_material_lambertian", "om_material_metal", "om_material_metal_fuzz", "om_material_dielectric",
     "om_mat4_identity", "om_mat4_translate", "om_mat4_scale", "om_mat4_rotate", "om_mat4_mul",
     "om_mat4_fast_homogenous_inverse", "om_camera_new", "om_world_create", "om_world_destroy", "om_world_clear",
     "om_world_add_sphere", "om_world_add_sphere_radius", "om_world_add_cube", "om_world_add_cube_length",
@@ -74,7 +74,13 @@ EXPORTS = [
     "om_render_device_pixels", "om_get_counters", "om_reset_counters", "om_set_counting", "om_set_pipeline",
     "om_set_tail_bounce", "om_set_streams", "om_set_timing", "om_get_kernel_times", "om_display_device", "om_display",
     "om_write_bmp", "om_write_ppm", "om_set_primary_lists",
+    "om_shard_capacity", "om_shard_pixels", "om_shard_assemble_host", "om_comm_unique_id", "om_comm_init_rank",
+    "om_comm_destroy", "om_render_shard", "om_gather_frame", "om_scatter_frame", "om_multi_create",
+    "om_multi_destroy", "om_multi_transport", "om_multi_ctx", "om_multi_upload_world", "om_multi_render",
+    "om_multi_last_error",
 ]
+OM_COMM_ID_BYTES = 128
+OM_TRANSPORT_RCCL, OM_TRANSPORT_LOCAL = 0, 1
 
 
 class OmError(RuntimeError):
@@ -105,6 +111,7 @@ def _load():
     mp = C.POINTER(om_material)
     sig = {
         "om_abi_version": (C.c_int32, []),
+        "om_build_id": (C.c_char_p, []),
         "om_material_lambertian": (om_material, [C.c_float] * 3),
         "om_material_metal": (om_material, [C.c_float] * 3),
         "om_material_metal_fuzz": (om_material, [C.c_float] * 4),
@@ -157,6 +164,22 @@ def _load():
         "om_write_bmp": (st, [C.c_char_p, vp, C.c_uint32, C.c_uint32]),
         "om_write_ppm": (st, [C.c_char_p, vp, C.c_uint32, C.c_uint32]),
         "om_set_primary_lists": (st, [vp, C.c_int32]),
+        "om_shard_capacity": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
+        "om_shard_pixels": (st, [C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, vp, C.c_uint32, C.POINTER(C.c_uint32)]),
+        "om_shard_assemble_host": (st, [C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(vp), vp]),
+        "om_comm_unique_id": (st, [vp]),
+        "om_comm_init_rank": (st, [vp, C.c_uint32, C.c_uint32, vp, C.POINTER(vp)]),
+        "om_comm_destroy": (None, [vp]),
+        "om_render_shard": (st, [vp, C.POINTER(om_camera), C.POINTER(om_render_params), vp, vp]),
+        "om_gather_frame": (st, [vp, vp, C.c_uint32, C.c_uint32, vp, vp]),
+        "om_scatter_frame": (st, [vp, vp, C.c_uint32, C.c_uint32, vp, vp]),
+        "om_multi_create": (st, [C.POINTER(C.c_int32), C.c_uint32, C.POINTER(vp)]),
+        "om_multi_destroy": (None, [vp]),
+        "om_multi_transport": (C.c_int32, [vp]),
+        "om_multi_ctx": (vp, [vp, C.c_uint32]),
+        "om_multi_upload_world": (st, [vp, vp]),
+        "om_multi_render": (st, [vp, C.POINTER(om_camera), C.POINTER(om_render_params), vp, vp]),
+        "om_multi_last_error": (C.c_char_p, [vp]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -166,6 +189,21 @@ def _load():
 
 
 lib = _load()
+
+
+def build_id():
+    """Source hash the loaded library was built from (om_build_id)."""
+    return lib.om_build_id().decode()
+
+
+def check_build_provenance():
+    """Raise if the loaded library was not built from the checked-out sources."""
+    from .build_id import source_hash
+    want, got = source_hash(), build_id()
+    if want != got:
+        raise OmError(f"{LIB_PATH} was built from other sources (om_build_id {got}, checked-out sources {want}): "
+                      "rebuild with __graft_entry__.build()")
+    return got
 
 
 def check(status, ctx=None):

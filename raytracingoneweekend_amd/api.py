@@ -358,9 +358,14 @@ class RenderStats(dict):
 
 
 def render(camera, world, max_depth, tmin, tmax, samples_per_pixel, image_width, image_height, pixels_box,
-           tid=0, assigned_thread=None, samples_atom=None, *, seed=1, march_steps=1024, adaptive=False,
+           tid=0, assigned_thread=None, samples_atom=None, *, seed=1, march_steps=1024, adaptive=True,
            sample_count=None):
     """render_thread::render (render_thread.rs:145-202) for the whole frame.
+
+    `adaptive` defaults to True, as the reference always retires a pixel once bad_avgs
+    reaches 5 (ThreadPixels::add_run, render_thread.rs:97-101,195-198) and credits its
+    untaken samples to samples_atom; pass adaptive=False for a fixed-spp render (the
+    BASELINE metric).
 
     The reference spawns num_cpus-1 threads with disjoint pixel sets (main.rs:200-214);
     here tid 0 renders every pixel on the device and other tids return at once, so a

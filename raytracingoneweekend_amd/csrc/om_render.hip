@@ -13,6 +13,7 @@
 // addresses (scalar loads) and stay L2/LDS resident.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <mutex>
@@ -27,6 +28,7 @@
 #include "om_tiles.h"
 #include "om_wavefront.h"
 #include "om_world.h"
+#include "om_internal.h"
 
 using namespace omd;
 
@@ -258,8 +260,11 @@ struct om_ctx {
     OmSceneDev scene{};
     bool have_world = false;
     int kernel = OM_KERNEL_AUTO;
-    DevBuf counters, jitter, stats, pixels, view_scratch, view_rgb;
-    uint64_t jitter_seed = 0; uint32_t jitter_spp = 0;
+    DevBuf counters, stats, pixels, view_scratch, view_rgb;
+    // jitter tables, one immutable device buffer per (seed, spp_total): a table that queued
+    // kernels may still read is never rewritten in place (most recent first, kMaxJitterTables)
+    struct JitterTable { uint64_t seed; uint32_t spp; DevBuf buf; };
+    std::vector<JitterTable> jitters;
     hipStream_t last_stream = nullptr;
     bool count_work = true;
     int pipeline = OM_PIPELINE_AUTO;
@@ -282,7 +287,8 @@ struct om_ctx {
     uint32_t frame_w = 0, frame_h = 0;
     ~om_ctx() {
         for (auto& b : scene_bufs) b.release();
-        counters.release(); jitter.release(); stats.release(); pixels.release(); frame_list.release();
+        for (auto& j : jitters) j.buf.release();
+        counters.release(); stats.release(); pixels.release(); frame_list.release();
         view_scratch.release(); view_rgb.release(); tile_off.release(); tile_idx.release();
         wf.release();
         timer.release();
@@ -324,9 +330,18 @@ om_status ensure(om_ctx* c, DevBuf& b, size_t n) {
     return OM_OK;
 }
 
-// jitter table render_thread.rs:164-174: ((s/2)&1, s&1) shuffled once (om-rng SplitMix64 Fisher-Yates)
-om_status prepare_jitter(om_ctx* c, uint64_t seed, uint32_t spp) {
-    if (c->jitter.p && c->jitter_seed == seed && c->jitter_spp == spp) return OM_OK;
+// jitter table render_thread.rs:164-174: ((s/2)&1, s&1) shuffled once (om-rng SplitMix64 Fisher-Yates).
+// Each (seed, spp) gets its own device buffer, written once before any kernel can read it,
+// so an asynchronous call with another seed never races a queued one.
+constexpr size_t kMaxJitterTables = 8;
+om_status prepare_jitter(om_ctx* c, uint64_t seed, uint32_t spp, const float2** out) {
+    *out = nullptr;
+    for (size_t i = 0; i < c->jitters.size(); ++i)
+        if (c->jitters[i].seed == seed && c->jitters[i].spp == spp) {
+            if (i) std::rotate(c->jitters.begin(), c->jitters.begin() + i, c->jitters.begin() + i + 1);
+            *out = (const float2*)c->jitters[0].buf.p;
+            return OM_OK;
+        }
     std::vector<float> jt(2 * (size_t)spp);
     for (uint32_t s = 0; s < spp; ++s) { jt[2 * s] = (float)((s / 2) & 1u); jt[2 * s + 1] = (float)(s & 1u); }
     auto mix = [](uint64_t z) {
@@ -341,11 +356,22 @@ om_status prepare_jitter(om_ctx* c, uint64_t seed, uint32_t spp) {
         std::swap(jt[2 * i], jt[2 * j]);
         std::swap(jt[2 * i + 1], jt[2 * j + 1]);
     }
-    om_status s = ensure(c, c->jitter, jt.size() * sizeof(float) + 16);
+    if (c->jitters.size() >= kMaxJitterTables) {      // evict the least recent once the device is idle
+        OM_HIP(c, hipDeviceSynchronize());
+        c->jitters.back().buf.release();
+        c->jitters.pop_back();
+    }
+    om_ctx::JitterTable t{seed, spp, DevBuf{}};
+    om_status s = ensure(c, t.buf, jt.size() * sizeof(float) + 16);
     if (s) return s;
-    OM_HIP(c, hipMemcpyAsync(c->jitter.p, jt.data(), jt.size() * sizeof(float), hipMemcpyHostToDevice, c->stream));
-    OM_HIP(c, hipStreamSynchronize(c->stream));  // jt is a host temporary
-    c->jitter_seed = seed; c->jitter_spp = spp;
+    const hipError_t e = hipMemcpyAsync(t.buf.p, jt.data(), jt.size() * sizeof(float), hipMemcpyHostToDevice, c->stream);
+    const hipError_t e2 = e == hipSuccess ? hipStreamSynchronize(c->stream) : e;   // jt is a host temporary
+    if (e2 != hipSuccess) {
+        t.buf.release();
+        return set_err(c, OM_ERR_DEVICE, std::string("jitter upload: ") + hipGetErrorString(e2));
+    }
+    c->jitters.insert(c->jitters.begin(), t);
+    *out = (const float2*)t.buf.p;
     return OM_OK;
 }
 
@@ -384,8 +410,9 @@ om_status ensure_tile_lists(om_ctx* c, const om_camera* cam, uint32_t W, uint32_
     if (!same) {
         omt::TileLists tl;
         const bool ok = omt::build(c->srec_box, *cam, W, H, tl);
-        c->tiles_valid = true; c->tiles_gen = c->world_gen; c->tiles_w = W; c->tiles_h = H; c->tiles_cam = *cam;
-        c->tiles_avg = ok ? tl.avg_per_pixel : -1.0;
+        // the cache keys are set only once the device lists are complete: a failed upload
+        // leaves tiles_valid false, so the next call rebuilds instead of reading stale lists
+        c->tiles_valid = false;
         c->tiles_use = false;
         if (ok) {
             om_status s = ensure(c, c->tile_off, tl.off.size() * 4u);
@@ -394,8 +421,9 @@ om_status ensure_tile_lists(om_ctx* c, const om_camera* cam, uint32_t W, uint32_
             OM_HIP(c, hipStreamSynchronize(stream));        // the previous lists may still be read
             OM_HIP(c, hipMemcpy(c->tile_off.p, tl.off.data(), tl.off.size() * 4u, hipMemcpyHostToDevice));
             if (!tl.idx.empty()) OM_HIP(c, hipMemcpy(c->tile_idx.p, tl.idx.data(), tl.idx.size() * 2u, hipMemcpyHostToDevice));
-            c->tiles_use = true;
         }
+        c->tiles_valid = true; c->tiles_gen = c->world_gen; c->tiles_w = W; c->tiles_h = H; c->tiles_cam = *cam;
+        c->tiles_avg = ok ? tl.avg_per_pixel : -1.0;
     }
     c->tiles_use = c->tiles_avg >= 0.0 &&
                    (c->primary_lists == OM_PRIMARY_LISTS_ON || c->tiles_avg <= kTileListMaxAvg);
@@ -406,7 +434,8 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
                  const uint32_t* dev_pixels, uint32_t n_pixels, hipStream_t stream) {
     // samples_per_pixel = 0: render()'s pass loop never runs (render_thread.rs:176), Stats untouched
     if (p->spp_total == 0 || p->sample_count == 0) return OM_OK;
-    om_status s = prepare_jitter(c, p->seed, p->spp_total);
+    const float2* jitter = nullptr;
+    om_status s = prepare_jitter(c, p->seed, p->spp_total, &jitter);
     if (s) return s;
     if (!c->counters.p) {
         s = ensure(c, c->counters, OMC_N * sizeof(unsigned long long));
@@ -456,7 +485,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     if (pipeline == OM_PIPELINE_WAVEFRONT) {
         omw::Launch L;
         L.S = c->scene; L.C = C; L.P = P;
-        L.jitter = (const float2*)c->jitter.p;
+        L.jitter = jitter;
         L.stats = dev_stats;
         L.counters = (unsigned long long*)c->counters.p;
         L.count = c->count_work;
@@ -496,7 +525,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         if (e != hipSuccess) return set_err(c, OM_ERR_DEVICE, err + ": " + hipGetErrorString(e));
         return OM_OK;
     }
-    const float2* jt = (const float2*)c->jitter.p;
+    const float2* jt = jitter;
     unsigned long long* ctr = (unsigned long long*)c->counters.p;
     const bool count = c->count_work;
     const int mk_ti = c->timer.begin(stream);
@@ -779,3 +808,10 @@ om_status om_reset_counters(om_ctx* c, void* stream) {
 }
 
 }  // extern "C"
+
+namespace omi {
+int ctx_device(const om_ctx* c) { return c->device; }
+hipStream_t ctx_stream(const om_ctx* c) { return c->stream; }
+om_status ctx_error(om_ctx* c, om_status code, const std::string& msg) { return set_err(c, code, msg); }
+om_status global_error(om_status code, const std::string& msg) { return set_err(nullptr, code, msg); }
+}  // namespace omi

@@ -1,57 +1,125 @@
-"""Pixel-tile sharding of a frame across ranks (one process per GPU) and the
-framebuffer gather.
+"""Multi-GPU frames: pixel-tile shards and the RCCL gather, over the C-ABI.
 
-Reference analogue: main.rs:172-189 deals 2730-pixel chunks round-robin to CPU
-threads.  Here 8x8 tiles (one wavefront each) are dealt round-robin to ranks, so
-every rank gets a spatially interleaved, cost-balanced share.  Pixels are
-independent and om-rng is keyed by (pixel, sample), so a sharded render is
-bit-identical to a single-device render.
+Reference analogue: main.rs:170-214 deals 2730-pixel chunks round-robin to num_cpus-1 render
+threads sharing one framebuffer.  Here 8x8 tiles (one wavefront each) are dealt round-robin to
+ranks (om_shard_pixels), every rank renders its tiles into a compact shard, and the shards are
+gathered to rank 0 with one RCCL group of send/recv (om_gather_frame) or, for one process
+driving several GPUs, inside om_multi_render.  Pixels are independent and om-rng is keyed by
+(pixel, sample), so a sharded frame is bit-identical to a single-device render.
+
+Everything here marshals arguments to libottomarcher.so; nothing is computed in Python.
 """
+import ctypes as C
+
 import numpy as np
 
-from ._lib import PIXEL_STATS_DTYPE
+from . import _lib as L
+from ._lib import PIXEL_STATS_DTYPE, check, lib
 
 TILE = 8
 
 
-def tile_pixels(width, height, rank, world_size):
-    """Row-major pixel indices of the tiles t with t % world_size == rank, tile-major,
-    each tile in lane order (lane = 8*y + x).  Out-of-frame lanes of edge tiles are dropped."""
-    tx, ty = (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
-    lane = np.arange(TILE * TILE)
-    lx, ly = lane % TILE, lane // TILE
-    tiles = np.arange(rank, tx * ty, world_size)
-    px = (tiles[:, None] % tx) * TILE + lx[None, :]
-    py = (tiles[:, None] // tx) * TILE + ly[None, :]
-    ok = (px < width) & (py < height)
-    return (py * width + px)[ok].astype(np.uint32)
-
-
 def shard_capacity(width, height, world_size):
-    """Upper bound of any rank's pixel count (equal-size buffers for the collective)."""
-    tx, ty = (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
-    return ((tx * ty + world_size - 1) // world_size) * TILE * TILE
+    """Pixels of the largest rank's shard (om_shard_capacity): every shard buffer's size."""
+    return int(lib.om_shard_capacity(int(width), int(height), int(world_size)))
+
+
+def tile_pixels(width, height, rank, world_size):
+    """Row-major pixel indices of rank's tiles (om_shard_pixels): tiles t with
+    t % world_size == rank in row-major tile order, each tile's in-frame pixels in lane order."""
+    cap = shard_capacity(width, height, world_size)
+    out = np.empty(max(cap, 1), dtype=np.uint32)
+    n = C.c_uint32()
+    check(lib.om_shard_pixels(int(width), int(height), int(rank), int(world_size), out.ctypes.data, cap, C.byref(n)))
+    return out[: n.value].copy()
 
 
 def assemble(width, height, shards):
-    """Scatter per-rank compact om_pixel_stats shards (rank order) back into a W*H frame."""
-    frame = np.zeros(width * height, dtype=PIXEL_STATS_DTYPE)
+    """Frame (om_pixel_stats[W*H]) from every rank's host shard in rank order (om_shard_assemble_host)."""
     ws = len(shards)
-    for r, sh in enumerate(shards):
-        idx = tile_pixels(width, height, r, ws)
-        frame[idx] = np.asarray(sh).view(PIXEL_STATS_DTYPE)[: idx.size]
+    arrs = [np.ascontiguousarray(np.asarray(s).view(np.uint8)).view(PIXEL_STATS_DTYPE) for s in shards]
+    ptrs = (C.c_void_p * ws)(*[a.ctypes.data for a in arrs])
+    frame = np.zeros(int(width) * int(height), dtype=PIXEL_STATS_DTYPE)
+    check(lib.om_shard_assemble_host(int(width), int(height), ws, ptrs, frame.ctypes.data))
     return frame
 
 
-def gather_frame(dist, stats_u8, width, height, rank, world_size, device=None):
-    """Gather every rank's compact uint8 stats tensor (torch) to rank 0 and assemble the
-    frame there (numpy om_pixel_stats[W*H]); other ranks return None.  One collective."""
-    import torch
-    cap = shard_capacity(width, height, world_size) * PIXEL_STATS_DTYPE.itemsize
-    send = torch.zeros(cap, dtype=torch.uint8, device=stats_u8.device if device is None else device)
-    send[: stats_u8.numel()] = stats_u8
-    bufs = [torch.empty_like(send) for _ in range(world_size)] if rank == 0 else None
-    dist.gather(send, bufs, dst=0)
-    if rank != 0:
-        return None
-    return assemble(width, height, [b.cpu().numpy() for b in bufs])
+def unique_id():
+    """om_comm_unique_id: the 128 bytes rank 0 hands to every rank before Comm()."""
+    buf = (C.c_uint8 * L.OM_COMM_ID_BYTES)()
+    check(lib.om_comm_unique_id(buf))
+    return bytes(buf)
+
+
+class Comm:
+    """One rank of a frame shard communicator (om_comm: RCCL over xGMI), bound to `ctx`'s device.
+    Every rank must construct it (it blocks until all ranks joined)."""
+
+    def __init__(self, ctx, world_size, rank, uid):
+        if len(uid) != L.OM_COMM_ID_BYTES:
+            raise ValueError("unique id must be OM_COMM_ID_BYTES long")
+        self.ctx, self.world_size, self.rank = ctx, int(world_size), int(rank)
+        self._c = C.c_void_p()
+        idbuf = (C.c_uint8 * L.OM_COMM_ID_BYTES).from_buffer_copy(uid)
+        check(lib.om_comm_init_rank(ctx, self.world_size, self.rank, idbuf, C.byref(self._c)), ctx)
+
+    def render_shard(self, cam, params, dev_shard_ptr, stream=None):
+        check(lib.om_render_shard(self._c, C.byref(cam.raw if hasattr(cam, "raw") else cam), C.byref(params),
+                                  C.c_void_p(dev_shard_ptr), C.c_void_p(stream)), self.ctx)
+
+    def gather_frame(self, dev_shard_ptr, width, height, dev_frame_ptr, stream=None):
+        check(lib.om_gather_frame(self._c, C.c_void_p(dev_shard_ptr), int(width), int(height),
+                                  C.c_void_p(dev_frame_ptr), C.c_void_p(stream)), self.ctx)
+
+    def scatter_frame(self, dev_frame_ptr, width, height, dev_shard_ptr, stream=None):
+        check(lib.om_scatter_frame(self._c, C.c_void_p(dev_frame_ptr), int(width), int(height),
+                                   C.c_void_p(dev_shard_ptr), C.c_void_p(stream)), self.ctx)
+
+    def close(self):
+        if getattr(self, "_c", None) and self._c.value:
+            lib.om_comm_destroy(self._c)
+            self._c = C.c_void_p()
+
+    def __del__(self):
+        self.close()
+
+
+class MultiFrame:
+    """One process driving several GPUs (om_multi): a ctx per device, tile shards, and the
+    gather (RCCL for distinct devices; device copies when a device repeats)."""
+
+    def __init__(self, devices, world, kernel="auto", pipeline="auto"):
+        devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
+        self._m = C.c_void_p()
+        st = lib.om_multi_create(devs, len(devices), C.byref(self._m))
+        if st != L.OM_OK:
+            raise L.OmError(f"om_multi_create failed ({st}): {lib.om_multi_last_error(None).decode()}")
+        self.n = len(devices)
+        self._check(lib.om_multi_upload_world(self._m, world.handle))
+        for r in range(self.n):
+            ctx = self.ctx(r)
+            check(lib.om_set_kernel(ctx, L.KERNELS[kernel]), ctx)
+            check(lib.om_set_pipeline(ctx, L.PIPELINES[pipeline]), ctx)
+
+    def _check(self, st):
+        if st != L.OM_OK:
+            raise L.OmError(f"ottomarcher multi error {st}: {lib.om_multi_last_error(self._m).decode()}")
+
+    @property
+    def transport(self):
+        return {L.OM_TRANSPORT_RCCL: "rccl", L.OM_TRANSPORT_LOCAL: "local"}[lib.om_multi_transport(self._m)]
+
+    def ctx(self, rank):
+        return C.c_void_p(lib.om_multi_ctx(self._m, rank))
+
+    def render(self, cam, params, dev_frame_ptr, stream=None):
+        self._check(lib.om_multi_render(self._m, C.byref(cam.raw), C.byref(params), C.c_void_p(dev_frame_ptr),
+                                        C.c_void_p(stream)))
+
+    def close(self):
+        if getattr(self, "_m", None) and self._m.value:
+            lib.om_multi_destroy(self._m)
+            self._m = C.c_void_p()
+
+    def __del__(self):
+        self.close()

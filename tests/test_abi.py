@@ -34,6 +34,16 @@ def test_library_is_gfx950_code_object(om):
     assert b"gfx950" in blob and b"render_kernel" in blob
 
 
+def test_build_id_matches_checked_out_sources(om):
+    """Build provenance: the library names the source hash it was built from (baked in at
+    link time by csrc/Makefile), which must be the hash of the sources in this tree."""
+    from raytracingoneweekend_amd import _lib
+    from raytracingoneweekend_amd.build_id import source_hash
+    assert re.fullmatch(r"[0-9a-f]{16}", _lib.build_id())
+    assert _lib.build_id() == source_hash()
+    assert _lib.check_build_provenance() == source_hash()
+
+
 def test_abi_version_and_struct_sizes(om):
     from raytracingoneweekend_amd import _lib
     assert _lib.lib.om_abi_version() == 2

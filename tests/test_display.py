@@ -133,7 +133,7 @@ def test_gpu_views_match_oracle(om, oracle, W, H):
     cam = om.default_camera(W / H)
     frozen = om.random_scene(0x5EED).freeze(cam)
     rendered = om.PixelsBox.new(W * H)
-    om.render(cam, frozen, 50, 0.001, 100.0, 3, W, H, rendered, seed=2)
+    om.render(cam, frozen, 50, 0.001, 100.0, 3, W, H, rendered, seed=2, adaptive=False)
     for name, st in (("rendered", rendered.pixels), ("adversarial", _adversarial(oracle, W, H, W * 31 + H))):
         for mode in range(7):
             prev = np.random.default_rng(mode).integers(0, 256, (H, W, 3), dtype=np.uint8)

@@ -1,7 +1,9 @@
-"""N>1 path on CPU: world_size-2 gloo ranks shard the frame by 8x8 tiles
-(raytracingoneweekend_amd.shard), render their tiles (CPU oracle stands in for the
-device here) and gather to rank 0 with one collective; the assembled frame must be
-bit-identical to a single-rank render (RNG keyed by pixel and sample, not by rank)."""
+"""N>1 path on CPU: world_size-2/3 gloo ranks take their 8x8-tile shards from the product's
+deal (om_shard_pixels), render them, send them to rank 0, and rank 0 assembles the frame with
+the product's om_shard_assemble_host; the frame must be bit-identical to a single-rank render
+(om-rng is keyed by pixel and sample, not by rank).  There is no GPU here, so the per-rank
+render is the CPU oracle's render_pixels and gloo carries the bytes RCCL carries on the GPU
+(om_gather_frame, tested on the GPU in test_multi_gpu.py)."""
 import os
 import socket
 
@@ -30,10 +32,16 @@ def _worker(rank, world_size, port, out_path):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world_size)
-    pix = shard.tile_pixels(W, H, rank, world_size)
+    pix = shard.tile_pixels(W, H, rank, world_size)                       # the product's tile deal
     st = O.render_pixels(O.random_scene(0x5EED), O.default_camera(W / H), O.params(W, H, SPP, seed=9), pix)
-    frame = shard.gather_frame(dist, torch.from_numpy(st.view(np.uint8).copy()), W, H, rank, world_size)
-    if rank == 0:
+    cap = shard.shard_capacity(W, H, world_size) * 40
+    send = torch.zeros(cap, dtype=torch.uint8)
+    send[: pix.size * 40] = torch.from_numpy(st.view(np.uint8).copy())
+    bufs = [torch.empty_like(send) for _ in range(world_size)] if rank == 0 else None
+    dist.gather(send, bufs, dst=0)
+    if rank == 0:                                                          # the product's assembly
+        sizes = [shard.tile_pixels(W, H, r, world_size).size for r in range(world_size)]
+        frame = shard.assemble(W, H, [b.numpy()[: n * 40] for b, n in zip(bufs, sizes)])
         np.save(out_path, frame.view(np.uint8))
     dist.barrier()
     dist.destroy_process_group()
@@ -48,6 +56,49 @@ def test_tile_sharded_gather_is_bit_identical(oracle, tmp_path, world_size):
     ref, _ = oracle.render(oracle.random_scene(0x5EED), oracle.default_camera(W / H), oracle.params(W, H, SPP, seed=9),
                            nthreads=2)
     assert np.array_equal(got, ref.view(np.uint8))
+
+
+def _deal_restated(w, h, rank, ws):
+    """Independent restatement of the deal: tiles t % ws == rank, row-major, lanes row-major."""
+    tx, ty = (w + 7) // 8, (h + 7) // 8
+    out = []
+    for t in range(rank, tx * ty, ws):
+        for lane in range(64):
+            px, py = (t % tx) * 8 + lane % 8, (t // tx) * 8 + lane // 8
+            if px < w and py < h:
+                out.append(py * w + px)
+    return np.array(out, dtype=np.uint32)
+
+
+def test_native_deal_matches_restatement():
+    from raytracingoneweekend_amd import shard
+    for (w, h) in [(37, 21), (8, 8), (1, 1), (3, 50), (64, 9)]:
+        for ws in (1, 2, 3, 8, 20):
+            for r in range(ws):
+                assert np.array_equal(shard.tile_pixels(w, h, r, ws), _deal_restated(w, h, r, ws)), (w, h, ws, r)
+
+
+def test_shard_argument_errors(om):
+    from raytracingoneweekend_amd import _lib as L
+    import ctypes as C
+    n = C.c_uint32()
+    assert L.lib.om_shard_pixels(16, 16, 2, 2, None, 0, C.byref(n)) == L.OM_ERR_INVALID      # rank >= nranks
+    assert L.lib.om_shard_pixels(16, 16, 0, 2, None, 0, C.byref(n)) == L.OM_ERR_INVALID      # no room
+    assert n.value == 128
+    assert L.lib.om_shard_capacity(16, 16, 0) == 0
+    assert L.lib.om_comm_init_rank(None, 2, 0, None, None) == L.OM_ERR_INVALID
+    assert L.lib.om_multi_create(None, 0, None) == L.OM_ERR_INVALID
+    assert L.lib.om_multi_transport(None) == -1
+
+
+def test_assemble_round_trip():
+    from raytracingoneweekend_amd import _lib as L
+    from raytracingoneweekend_amd import shard
+    w, h, ws = 45, 19, 3
+    rng = np.random.default_rng(1)
+    frame = rng.integers(0, 256, size=w * h * 40, dtype=np.uint8).view(L.PIXEL_STATS_DTYPE)
+    shards = [frame[shard.tile_pixels(w, h, r, ws)] for r in range(ws)]
+    assert np.array_equal(shard.assemble(w, h, shards).view(np.uint8), frame.view(np.uint8))
 
 
 def test_tiles_partition_the_frame():

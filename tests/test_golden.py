@@ -49,7 +49,7 @@ def test_oracle_reproduces_images(oracle):
 def _gpu_render(om, world, cam, W, H, spp, seed, kernel, march_steps=1024):
     fz = world.freeze(cam, kernel=kernel)
     pix = om.PixelsBox.new(W * H)
-    om.render(cam, fz, 50, 0.001, 100.0, spp, W, H, pix, seed=seed, march_steps=march_steps)
+    om.render(cam, fz, 50, 0.001, 100.0, spp, W, H, pix, seed=seed, march_steps=march_steps, adaptive=False)
     return pix.pixels.view(np.uint8).reshape(-1, 40)
 
 

@@ -102,10 +102,10 @@ def test_progressive_calls_equal_single_call(om, pipeline):
     cam = om.default_camera(W / H)
     fz = world.freeze(cam, pipeline=pipeline)
     a = om.PixelsBox.new(W * H)
-    om.render(cam, fz, 50, 0.001, 100.0, 8, W, H, a, seed=5)
+    om.render(cam, fz, 50, 0.001, 100.0, 8, W, H, a, seed=5, adaptive=False)
     b = om.PixelsBox.new(W * H)
     for _ in range(4):
-        om.render(cam, fz, 50, 0.001, 100.0, 8, W, H, b, seed=5, sample_count=2)
+        om.render(cam, fz, 50, 0.001, 100.0, 8, W, H, b, seed=5, sample_count=2, adaptive=False)
     nb, msg = compare_stats(b.pixels, a.pixels, "progressive")
     assert nb == 0, msg
 
@@ -141,7 +141,7 @@ def test_counters_consistent(om, pipeline):
     for k in KERNELS:
         fz = world.freeze(cam, kernel=k, pipeline=pipeline)
         pix = om.PixelsBox.new(W * H)
-        c = om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=2)
+        c = om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=2, adaptive=False)
         assert c["samples"] == W * H * SPP
         assert c["segments"] >= c["samples"]
         if k == "brute":
@@ -159,7 +159,7 @@ def test_counting_build_is_bit_identical(om, kernel):
         fz = world.freeze(cam, kernel=kernel[0], pipeline=kernel[1])
         L.check(L.lib.om_set_counting(fz.ctx, count), fz.ctx)
         pix = om.PixelsBox.new(W * H)
-        om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=4)
+        om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=4, adaptive=False)
         out.append(pix.pixels.copy())
     nb, msg = compare_stats(out[1], out[0], f"count/{kernel}")
     assert nb == 0, msg
@@ -177,7 +177,7 @@ def test_pixel_list_shard_equals_full_frame(om, kernel):
     cam = om.default_camera(W / H)
     full = om.PixelsBox.new(W * H)
     fz = world.freeze(cam, kernel=kernel)
-    om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, full, seed=6)
+    om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, full, seed=6, adaptive=False)
     shards = []
     p = om.make_params(50, 0.001, 100.0, SPP, W, H, seed=6)
     for r in range(3):
@@ -203,7 +203,7 @@ def test_tail_bounce_is_bit_identical(om, oracle, tail):
     fz = world.freeze(cam, kernel="auto", pipeline="wavefront")
     L.check(L.lib.om_set_tail_bounce(fz.ctx, tail), fz.ctx)
     pix = om.PixelsBox.new(W * H)
-    c = om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=9)
+    c = om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=9, adaptive=False)
     p = oracle.params(W, H, SPP, max_depth=50, seed=9)
     exp, _ = oracle.render(oracle.random_scene(0x5EED, with_torus=True), oracle.default_camera(W / H), p)
     nb, msg = compare_stats(pix.pixels, exp, f"tail{tail}")
@@ -245,7 +245,7 @@ def _render_lists(om, world, cam, W, H, spp, lists, seed=12, march_steps=1024):
     fz = world.freeze(cam, pipeline="wavefront")
     L.check(L.lib.om_set_primary_lists(fz.ctx, lists), fz.ctx)
     pix = om.PixelsBox.new(W * H)
-    om.render(cam, fz, 50, 0.001, 100.0, spp, W, H, pix, seed=seed, march_steps=march_steps)
+    om.render(cam, fz, 50, 0.001, 100.0, spp, W, H, pix, seed=seed, march_steps=march_steps, adaptive=False)
     return pix.pixels
 
 
@@ -288,8 +288,8 @@ def test_concurrent_batches_are_bit_identical(om, oracle, streams):
     L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
     L.check(L.lib.om_set_timing(fz.ctx, 1 + streams % 2), fz.ctx)
     pix = om.PixelsBox.new(W * H)
-    om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=4, sample_count=3)
-    om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=4, sample_count=9)   # 7 taken, 2 skipped
+    om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=4, sample_count=3, adaptive=False)
+    om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=4, sample_count=9, adaptive=False)   # 7 taken, 2 skipped
     kt = L.om_kernel_times()
     L.check(L.lib.om_get_kernel_times(fz.ctx, C.byref(kt)), fz.ctx)
     L.check(L.lib.om_set_timing(fz.ctx, 0), fz.ctx)
@@ -351,9 +351,58 @@ def test_zero_samples_and_empty_frames(om):
     cam = om.default_camera(W / H)
     fz = world.freeze(cam)
     pix = om.PixelsBox.new(W * H)
-    om.render(cam, fz, 50, 0.001, 100.0, 4, W, H, pix, seed=3, sample_count=2)
+    om.render(cam, fz, 50, 0.001, 100.0, 4, W, H, pix, seed=3, sample_count=2, adaptive=False)
     before = pix.pixels.copy()
-    om.render(cam, fz, 50, 0.001, 100.0, 0, W, H, pix, seed=3)
+    om.render(cam, fz, 50, 0.001, 100.0, 0, W, H, pix, seed=3, adaptive=False)
     assert np.array_equal(before.view(np.uint8), pix.pixels.view(np.uint8))
     with pytest.raises(L.OmError, match="width/height"):
-        om.render(cam, fz, 50, 0.001, 100.0, 4, 0, H, om.PixelsBox.new(0), seed=3)
+        om.render(cam, fz, 50, 0.001, 100.0, 4, 0, H, om.PixelsBox.new(0), seed=3, adaptive=False)
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_async_calls_with_different_seeds_on_one_stream(om, oracle, pipeline):
+    """Two om_render_device calls queued back to back on one user stream with different seeds
+    and spp_total (so different jitter tables), synchronised once at the end: each frame ==
+    the oracle.  Before r02 the second call rewrote the ctx's one jitter table while the first
+    call's kernels could still read it."""
+    import ctypes as C
+    import torch
+    from raytracingoneweekend_amd import _lib as L
+    W, H = 40, 24
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam, pipeline=pipeline)
+    s = torch.cuda.Stream()
+    cases = [(31, 6), (32, 10), (33, 6)]
+    frames = [torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda") for _ in cases]
+    torch.cuda.synchronize()
+    for (seed, spp), st in zip(cases, frames):
+        p = om.make_params(50, 0.001, 100.0, spp, W, H, seed=seed)
+        L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()),
+                                       C.c_void_p(s.cuda_stream)), fz.ctx)
+    s.synchronize()
+    for (seed, spp), st in zip(cases, frames):
+        exp, _ = oracle.render(oracle.random_scene(0x5EED), oracle.default_camera(W / H),
+                               oracle.params(W, H, spp, seed=seed))
+        got = st.cpu().numpy().view(L.PIXEL_STATS_DTYPE)
+        nb, msg = compare_stats(got, exp, f"async seed {seed}/{pipeline}")
+        assert nb == 0, msg
+
+
+def test_python_render_defaults_to_reference_adaptive(om, oracle):
+    """api.render() with no `adaptive` argument retires pixels like the reference's
+    render threads (ThreadPixels::add_run is unconditional, render_thread.rs:97-101) and
+    credits samples_atom with the untaken samples (render_thread.rs:196-198)."""
+    W, H, SPP = 32, 24, 24
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam)
+    pix = om.PixelsBox.new(W * H)
+    atom = [0]
+    om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, samples_atom=atom, seed=14)
+    exp, ctr = oracle.render(oracle.random_scene(0x5EED), oracle.default_camera(W / H),
+                             oracle.params(W, H, SPP, seed=14, adaptive=True))
+    nb, msg = compare_stats(pix.pixels, exp, "default adaptive")
+    assert nb == 0, msg
+    assert pix.pixels["n"].min() < SPP
+    assert atom[0] == W * H * SPP

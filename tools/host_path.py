@@ -28,11 +28,11 @@ def main():
     cam = om.default_camera(W / H)
     fz = om.random_scene(0x5EED).freeze(cam)
     pix = om.PixelsBox.new(W * H)
-    om.render(cam, fz, 50, 0.001, 100.0, 64, W, H, pix, seed=1, sample_count=16)          # warm-up
+    om.render(cam, fz, 50, 0.001, 100.0, 64, W, H, pix, seed=1, sample_count=16, adaptive=False)          # warm-up
     pix = om.PixelsBox.new(W * H)
     t0 = time.perf_counter()
     for _ in range(4):
-        om.render(cam, fz, 50, 0.001, 100.0, 64, W, H, pix, seed=1, sample_count=16)
+        om.render(cam, fz, 50, 0.001, 100.0, 64, W, H, pix, seed=1, sample_count=16, adaptive=False)
     dt = time.perf_counter() - t0
     assert int(pix.pixels["n"].min()) == 64
     out["c1_host_path"] = {"msamples_s": round(W * H * 64 / dt / 1e6, 1), "calls": 4, "spp_per_call": 16,

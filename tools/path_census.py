@@ -14,7 +14,7 @@ fz = world.freeze(cam)
 prev, out = 0, []
 for k in range(1, 51):
     pix = om.PixelsBox.new(W * H)
-    c = om.render(cam, fz, k, 0.001, 100.0, SPP, W, H, pix, seed=1)
+    c = om.render(cam, fz, k, 0.001, 100.0, SPP, W, H, pix, seed=1, adaptive=False)
     out.append(c["segments"] - prev)
     prev = c["segments"]
 n = W * H * SPP
