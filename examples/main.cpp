@@ -8,11 +8,15 @@
 // Instead of the SDL window (out of scope), every draw_to_sdl view (keys 0-6) is saved the
 // way F12 saves the window (main.rs:473-476).
 //
-//   make -C examples && examples/ottomarcher_main [--width 1000] [--spp 200] [--fixed] [--out DIR]
+// --gpus N spreads the frame over devices 0..N-1 (MultiFrame: 8x8 tiles dealt round-robin,
+// shards gathered over RCCL), still from render thread 0.
+//
+//   make -C examples && examples/ottomarcher_main [--width 1000] [--spp 200] [--fixed] [--gpus N] [--out DIR]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <filesystem>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -31,6 +35,7 @@ static void print_progress(double progress) {                                   
 int main(int argc, char** argv) {
     uint32_t image_width = 1000, samples_per_pixel = 200, max_depth = 50;                       // main.rs:126,145-146
     bool adaptive = true, torus = false;
+    int gpus = 1;
     std::string out = "out";
     for (int i = 1; i < argc; ++i) {
         const std::string a = argv[i];
@@ -44,7 +49,8 @@ int main(int argc, char** argv) {
         else if (a == "--fixed") adaptive = false;           // every pixel takes every sample (bench metric)
         else if (a == "--torus") torus = true;               // main.rs:73-81 block
         else if (a == "--out") out = next();
-        else { std::fprintf(stderr, "usage: %s [--width N] [--spp N] [--max-depth N] [--fixed] [--torus] [--out DIR]\n", argv[0]); return 2; }
+        else if (a == "--gpus") gpus = std::atoi(next());
+        else { std::fprintf(stderr, "usage: %s [--width N] [--spp N] [--max-depth N] [--fixed] [--torus] [--gpus N] [--out DIR]\n", argv[0]); return 2; }
     }
     try {
         // IMAGE (main.rs:124-130)
@@ -59,6 +65,12 @@ int main(int argc, char** argv) {
         std::atomic<uint64_t> samples_atomic{0};                                                 // main.rs:148-149
         const FrozenHittableList frozen = world.freeze(camera);   // main.rs:198 (before the log thread: a throw
                                                                   // must not leave a joinable thread behind)
+        std::unique_ptr<MultiFrame> multi;
+        if (gpus > 1) {
+            std::vector<int32_t> devices;
+            for (int d = 0; d < gpus; ++d) devices.push_back(d);
+            multi = std::make_unique<MultiFrame>(world, devices);
+        }
 
         const uint64_t total_samples = (uint64_t)image_size * samples_per_pixel;
         std::atomic<bool> quit{false};
@@ -87,8 +99,14 @@ int main(int argc, char** argv) {
         for (uint32_t i = 0; i < num_threads; ++i) {                                             // main.rs:200-214
             handlers.emplace_back([&, i]() {
                 try {
-                    render(camera, frozen, max_depth, 0.001f, 100.0f, samples_per_pixel, image_width, image_height,
-                           pixels_box, i, assigned_thread, samples_atomic, opt);
+                    if (multi) {   // thread 0 drives every GPU; the others return, as in render()
+                        if (i == 0)
+                            multi->render(camera, max_depth, 0.001f, 100.0f, samples_per_pixel, image_width,
+                                          image_height, pixels_box, samples_atomic, opt);
+                    } else {
+                        render(camera, frozen, max_depth, 0.001f, 100.0f, samples_per_pixel, image_width,
+                               image_height, pixels_box, i, assigned_thread, samples_atomic, opt);
+                    }
                 } catch (const std::exception& e) {
                     errors[i] = e.what();
                 }

@@ -190,9 +190,15 @@ const char* om_last_error(const om_ctx* ctx);      /* ctx may be NULL: last glob
 om_status om_upload_world(om_ctx* ctx, const om_world* w);
 om_status om_set_kernel(om_ctx* ctx, int32_t kernel);
 /* Host framebuffer path: `stats` is caller-owned W*H, read and written in place
- * (like PixelsBox, main.rs:192).  Includes the PCIe copies. */
+ * (like PixelsBox, main.rs:192).  Includes the PCIe copies: 40 B per pixel each way per
+ * call, at DMA speed when the buffer is page-locked (om_host_register), else staged by the
+ * runtime.  Prefer few calls per frame (om_progress reports progress inside a call). */
 om_status om_render(om_ctx* ctx, const om_camera* cam, const om_render_params* p, om_pixel_stats* stats,
                     om_counters* counters /* optional */);
+/* Page-lock a caller-owned host buffer (e.g. the framebuffer) so om_render's copies run as
+ * DMA at full PCIe speed; the buffer must stay allocated until om_host_unregister. */
+om_status om_host_register(void* p, size_t bytes);
+om_status om_host_unregister(void* p);
 /* Device framebuffer path: `dev_stats` is device memory (W*H om_pixel_stats) on ctx's
  * device; `stream` is a hipStream_t (NULL = ctx's own stream).  Asynchronous:
  * returns after enqueue; the caller synchronises the stream.  Calls queued back to back
@@ -210,6 +216,16 @@ om_status om_render_device_pixels(om_ctx* ctx, const om_camera* cam, const om_re
  * ctx's stream and the stream of the last launch. */
 om_status om_get_counters(om_ctx* ctx, om_counters* out);
 om_status om_reset_counters(om_ctx* ctx, void* stream);
+/* Live progress: the reference's samples_atom (render_thread.rs:196-198), which main.rs's
+ * log thread and display poll while the render threads run (main.rs:151-168, 371-377).
+ * om_progress returns a host word the library keeps pinned; every later render call on ctx
+ * adds its credited samples to it (each sample taken, plus a retiring pixel's untaken ones in
+ * adaptive calls) as each batch of the call is accumulated, so it advances while a call runs.
+ * Any host thread may read it without synchronising; it only grows.  After the call's stream
+ * is synchronised it has grown by exactly the call's om_counters.credited.  om_reset_progress
+ * zeroes it (synchronises the device).  NULL on error. */
+const volatile uint64_t* om_progress(om_ctx* ctx);
+om_status om_reset_progress(om_ctx* ctx);
 /* Work counting on (default) / off.  Off selects kernel builds with the counters
  * compiled out (fewer registers); results are bit-identical either way. */
 om_status om_set_counting(om_ctx* ctx, int32_t enable);
@@ -354,6 +370,11 @@ om_status om_multi_upload_world(om_multi* m, const om_world* w);
  * synchronising it covers the whole call. */
 om_status om_multi_render(om_multi* m, const om_camera* cam, const om_render_params* p, om_pixel_stats* dev_frame,
                           void* stream);
+/* Host framebuffer form (like om_render): `stats` (W*H, caller-owned host memory) is copied
+ * to devices[0], rendered across the ranks and copied back; synchronous.  `counters`
+ * (optional) sums every rank's work counters of this call. */
+om_status om_multi_render_host(om_multi* m, const om_camera* cam, const om_render_params* p, om_pixel_stats* stats,
+                               om_counters* counters);
 const char* om_multi_last_error(const om_multi* m);
 
 #ifdef __cplusplus

@@ -26,10 +26,12 @@
 #define OTTOMARCHER_HPP
 
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -303,12 +305,12 @@ struct PixelsBox {
 
 // What the Rust signature cannot carry.  `adaptive` defaults to the reference's behaviour:
 // render() always retires converged pixels (Stats::add's bad_avgs rule, render_thread.rs:31-38,
-// 97-101); the benchmark's fixed-spp metric turns it off.  `samples_per_call` splits the frame
-// into progressive passes so `samples_atom` advances while the device works (the reference
-// credits every sample, render_thread.rs:196-198).  `seed` keys om-rng (replaces thread_rng).
+// 97-101); the benchmark's fixed-spp metric turns it off.  `samples_per_call` (0 = the whole
+// frame in one call) splits the frame into progressive calls; progress does not need it:
+// samples_atom advances while a call runs (om_progress).  `seed` keys om-rng (replaces thread_rng).
 struct RenderOptions {
     bool adaptive = true;
-    uint32_t samples_per_call = 16;
+    uint32_t samples_per_call = 0;
     uint64_t seed = 1;
     uint32_t march_steps = 1024;   // hits.rs:292
 };
@@ -316,7 +318,11 @@ struct RenderOptions {
 // render_thread::render (render_thread.rs:145-202).  The reference calls it from num_cpus-1
 // threads with disjoint pixel sets (main.rs:200-214); here tid 0 renders every pixel on the
 // device and the other tids return at once, so main.rs's thread loop stays correct.
-// `assigned_thread` is accepted for signature parity and validated for size.
+// `assigned_thread` is accepted for signature parity and validated for size.  samples_atom
+// receives the reference's credit (render_thread.rs:196-198) live: a poller copies the
+// device-fed progress word (om_progress) into it every millisecond while the calls run, the
+// way main.rs's log thread polls the atomic (main.rs:151-168).  The framebuffer is page-locked
+// for the duration (om_host_register) so the per-call copies run at DMA speed.
 inline void render(const Camera& camera, const FrozenHittableList& world, uint32_t max_depth, float tmin, float tmax,
                    uint32_t samples_per_pixel, uint32_t image_width, uint32_t image_height, PixelsBox pixels_box,
                    uint32_t tid, const std::vector<uint32_t>& assigned_thread, std::atomic<uint64_t>& samples_atom,
@@ -326,9 +332,27 @@ inline void render(const Camera& camera, const FrozenHittableList& world, uint32
         throw Error(OM_ERR_INVALID, "ottomarcher: render: pixels must hold image_width*image_height entries");
     if (!assigned_thread.empty() && assigned_thread.size() != image_size)
         throw Error(OM_ERR_INVALID, "ottomarcher: render: assigned_thread must hold image_width*image_height entries");
-    if (tid != 0) return;
+    if (tid != 0 || samples_per_pixel == 0) return;
+    const volatile uint64_t* prog = om_progress(world.ctx());
+    if (!prog) throw Error(OM_ERR_DEVICE, std::string("ottomarcher: ") + om_last_error(world.ctx()));
+    const uint64_t p0 = *prog;
+    uint64_t credited = 0;                  // progress already added to samples_atom
+    auto publish = [&]() {
+        const uint64_t v = *prog - p0;
+        if (v > credited) { samples_atom.fetch_add(v - credited, std::memory_order_relaxed); credited = v; }
+    };
+    void* const buf = pixels_box.pixels->data();
+    const bool pinned = image_size && om_host_register(buf, image_size * sizeof(Pixel)) == OM_OK;
+    std::atomic<bool> stop{false};
+    std::thread poller([&]() {
+        while (!stop.load(std::memory_order_relaxed)) {
+            publish();
+            std::this_thread::sleep_for(std::chrono::milliseconds(1));
+        }
+    });
+    om_status st = OM_OK;
     const uint32_t per_call = opt.samples_per_call ? opt.samples_per_call : samples_per_pixel;
-    for (uint32_t done = 0; done < samples_per_pixel; done += per_call) {
+    for (uint32_t done = 0; done < samples_per_pixel && st == OM_OK; done += per_call) {
         om_render_params p{};
         p.width = image_width;
         p.height = image_height;
@@ -341,11 +365,57 @@ inline void render(const Camera& camera, const FrozenHittableList& world, uint32
         p.march_steps = opt.march_steps;
         p.adaptive = opt.adaptive ? 1u : 0u;
         p.seed = opt.seed;
-        om_counters c{};
-        check(om_render(world.ctx(), &camera.raw, &p, pixels_box.pixels->data(), &c), world.ctx());
-        samples_atom.fetch_add(c.credited, std::memory_order_relaxed);
+        st = om_render(world.ctx(), &camera.raw, &p, pixels_box.pixels->data(), nullptr);
     }
+    stop = true;
+    poller.join();
+    publish();                              // the calls are synchronous: the word is final
+    if (pinned) (void)om_host_unregister(buf);
+    check(st, world.ctx());
 }
+
+// The render threads of main.rs:170-214 spread over GPUs: a ctx per device, 8x8 tiles dealt
+// round-robin to them, the shards gathered into the caller's framebuffer (om_multi_*; RCCL
+// between distinct devices).  render() has render_thread::render's meaning for the whole frame.
+class MultiFrame {
+public:
+    MultiFrame(const HittableList& world, const std::vector<int32_t>& devices) {
+        check(om_multi_create(devices.data(), (uint32_t)devices.size(), &m_));
+        const om_status s = om_multi_upload_world(m_, world.handle());
+        if (s != OM_OK) {
+            Error e(s, std::string("ottomarcher: ") + om_multi_last_error(m_));
+            om_multi_destroy(m_);
+            throw e;
+        }
+    }
+    ~MultiFrame() { if (m_) om_multi_destroy(m_); }
+    MultiFrame(const MultiFrame&) = delete;
+    MultiFrame& operator=(const MultiFrame&) = delete;
+    int32_t transport() const { return om_multi_transport(m_); }
+    om_ctx* ctx(uint32_t rank) const { return om_multi_ctx(m_, rank); }
+    void render(const Camera& camera, uint32_t max_depth, float tmin, float tmax, uint32_t samples_per_pixel,
+                uint32_t image_width, uint32_t image_height, PixelsBox pixels_box, std::atomic<uint64_t>& samples_atom,
+                const RenderOptions& opt = RenderOptions()) {
+        const uint64_t image_size = (uint64_t)image_width * image_height;
+        if (!pixels_box.pixels || pixels_box.pixels->size() != image_size)
+            throw Error(OM_ERR_INVALID, "ottomarcher: MultiFrame::render: pixels must hold image_width*image_height entries");
+        const uint32_t per_call = opt.samples_per_call ? opt.samples_per_call : samples_per_pixel;
+        for (uint32_t done = 0; done < samples_per_pixel; done += per_call) {
+            om_render_params p{};
+            p.width = image_width; p.height = image_height; p.spp_total = samples_per_pixel; p.sample_begin = done;
+            p.sample_count = samples_per_pixel - done < per_call ? samples_per_pixel - done : per_call;
+            p.max_depth = max_depth; p.tmin = tmin; p.tmax = tmax; p.march_steps = opt.march_steps;
+            p.adaptive = opt.adaptive ? 1u : 0u; p.seed = opt.seed;
+            om_counters c{};
+            const om_status s = om_multi_render_host(m_, &camera.raw, &p, pixels_box.pixels->data(), &c);
+            if (s != OM_OK) throw Error(s, std::string("ottomarcher: ") + om_multi_last_error(m_));
+            samples_atom.fetch_add(c.credited, std::memory_order_relaxed);
+        }
+    }
+
+private:
+    om_multi* m_ = nullptr;
+};
 
 // draw_to_sdl views (main.rs:360-437) and the F12 save (main.rs:473-476), headless.
 inline std::vector<uint8_t> display(const FrozenHittableList& world, const std::vector<Pixel>& pixels, uint32_t width,

@@ -77,7 +77,8 @@ EXPORTS = [
     "om_shard_capacity", "om_shard_pixels", "om_shard_assemble_host", "om_comm_unique_id", "om_comm_init_rank",
     "om_comm_destroy", "om_render_shard", "om_gather_frame", "om_scatter_frame", "om_multi_create",
     "om_multi_destroy", "om_multi_transport", "om_multi_ctx", "om_multi_upload_world", "om_multi_render",
-    "om_multi_last_error",
+    "om_multi_last_error", "om_progress", "om_reset_progress", "om_host_register", "om_host_unregister",
+    "om_multi_render_host",
 ]
 OM_COMM_ID_BYTES = 128
 OM_TRANSPORT_RCCL, OM_TRANSPORT_LOCAL = 0, 1
@@ -180,6 +181,11 @@ def _load():
         "om_multi_upload_world": (st, [vp, vp]),
         "om_multi_render": (st, [vp, C.POINTER(om_camera), C.POINTER(om_render_params), vp, vp]),
         "om_multi_last_error": (C.c_char_p, [vp]),
+        "om_progress": (C.POINTER(C.c_uint64), [vp]),
+        "om_reset_progress": (st, [vp]),
+        "om_host_register": (st, [vp, C.c_size_t]),
+        "om_host_unregister": (st, [vp]),
+        "om_multi_render_host": (st, [vp, C.POINTER(om_camera), C.POINTER(om_render_params), vp, C.POINTER(om_counters)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -332,10 +332,24 @@ class PixelsBox:
 
     def __init__(self, image_size):
         self.pixels = np.zeros(int(image_size), dtype=L.PIXEL_STATS_DTYPE)
+        self._pinned = None
 
     @staticmethod
     def new(image_size):
         return PixelsBox(image_size)
+
+    def pin(self):
+        """Page-lock the framebuffer (om_host_register) so render()'s copies run as DMA; kept
+        until the box dies.  Done by render() on first use (needs a HIP device)."""
+        if self._pinned is None and self.pixels.nbytes:
+            check(lib.om_host_register(self.pixels.ctypes.data, self.pixels.nbytes))
+            self._pinned = self.pixels.ctypes.data
+        return self
+
+    def __del__(self):
+        if getattr(self, "_pinned", None):
+            lib.om_host_unregister(self._pinned)
+            self._pinned = None
 
 
 def make_params(max_depth, tmin, tmax, samples_per_pixel, image_width, image_height, sample_count=None,
@@ -376,6 +390,8 @@ def render(camera, world, max_depth, tmin, tmax, samples_per_pixel, image_width,
         return None
     p = make_params(max_depth, tmin, tmax, samples_per_pixel, image_width, image_height,
                     sample_count=sample_count, seed=seed, march_steps=march_steps, adaptive=adaptive)
+    if isinstance(pixels_box, PixelsBox) and p.width * p.height > 0:
+        pixels_box.pin()
     buf = pixels_box.pixels if isinstance(pixels_box, PixelsBox) else pixels_box
     if buf.dtype != L.PIXEL_STATS_DTYPE or buf.size != p.width * p.height or not buf.flags["C_CONTIGUOUS"]:
         raise ValueError("pixels must be a contiguous W*H om_pixel_stats array")

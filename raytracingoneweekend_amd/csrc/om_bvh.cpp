@@ -344,17 +344,17 @@ void build_bvh4(FrozenWorld& fw) {
         return dx * dy + dy * dz + dz * dx;
     };
     struct Rec {
-        FrozenWorld& fw; decltype(kids)& kids; decltype(area)& area;
+        FrozenWorld& fw; decltype(kids)& kids_of; decltype(area)& area_of;
         uint32_t go(uint32_t n2, uint32_t depth) {
             std::vector<Ch> ch(2);
-            kids(n2, ch.data());
+            kids_of(n2, ch.data());
             while (ch.size() < 4) {
                 int best = -1; double ba = -1.0;
                 for (size_t i = 0; i < ch.size(); ++i)
-                    if (!(ch[i].code & OM_LEAF) && area(ch[i]) > ba) { ba = area(ch[i]); best = (int)i; }
+                    if (!(ch[i].code & OM_LEAF) && area_of(ch[i]) > ba) { ba = area_of(ch[i]); best = (int)i; }
                 if (best < 0) break;
                 Ch two[2];
-                kids(ch[best].code, two);
+                kids_of(ch[best].code, two);
                 ch[best] = two[0];
                 ch.insert(ch.begin() + best + 1, two[1]);
             }

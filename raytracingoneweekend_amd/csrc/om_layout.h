@@ -185,7 +185,10 @@ struct OmParamsDev {
     uint64_t skey;                     // mix64(seed + K) (om-rng v2 path key)
     uint32_t n_pixels;                 // pixels this launch covers
     uint32_t tiles_x;                  // 8x8 tiles per row (full-frame mapping)
+    uint32_t progress;                 // 1: add credited samples to counters[OMC_PROGRESS] (om_progress)
 };
 
-// Counter slots (om_counters order)
+// Counter slots (om_counters order); OMC_PROGRESS (the live progress word, om_progress) sits
+// after them and is not cleared by om_reset_counters
 enum { OMC_SAMPLES = 0, OMC_SEGMENTS, OMC_PRIM_TESTS, OMC_PRE_TESTS, OMC_MARCH, OMC_CREDITED, OMC_N };
+enum { OMC_PROGRESS = OMC_N, OMC_SLOTS };

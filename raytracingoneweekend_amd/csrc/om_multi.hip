@@ -23,29 +23,15 @@
 
 #include "../../include/ottomarcher.h"
 #include "om_internal.h"
+#include "om_shard.h"
+
+using oms::capacity;
+using oms::deal;
 
 namespace {
 
-constexpr uint32_t kTile = 8;
 constexpr uint32_t kWords = sizeof(om_pixel_stats) / 8;   // 5 u64 words per pixel
 static_assert(sizeof(om_pixel_stats) == 40, "om_pixel_stats layout");
-
-uint64_t n_tiles(uint32_t w, uint32_t h) { return (uint64_t)((w + kTile - 1) / kTile) * ((h + kTile - 1) / kTile); }
-
-uint32_t capacity(uint32_t w, uint32_t h, uint32_t nranks) {
-    return (uint32_t)((n_tiles(w, h) + nranks - 1) / nranks * kTile * kTile);
-}
-
-// rank's pixels: tiles t = rank, rank + nranks, ... in row-major tile order, lane order inside
-void deal(uint32_t w, uint32_t h, uint32_t rank, uint32_t nranks, std::vector<uint32_t>& out) {
-    out.clear();
-    const uint32_t tx = (w + kTile - 1) / kTile;
-    for (uint64_t t = rank; t < n_tiles(w, h); t += nranks)
-        for (uint32_t l = 0; l < kTile * kTile; ++l) {
-            const uint32_t px = (uint32_t)(t % tx) * kTile + (l % kTile), py = (uint32_t)(t / tx) * kTile + l / kTile;
-            if (px < w && py < h) out.push_back(py * w + px);
-        }
-}
 
 // one lane per 8-B word: the shard side is read/written fully coalesced; the frame side in
 // runs of 8 pixels (320 B) per tile row
@@ -154,36 +140,6 @@ om_status check_frame(om_ctx* ctx, uint32_t W, uint32_t H) {
 }  // namespace
 
 extern "C" {
-
-uint32_t om_shard_capacity(uint32_t width, uint32_t height, uint32_t nranks) {
-    if (nranks == 0) return 0;
-    return capacity(width, height, nranks);
-}
-
-om_status om_shard_pixels(uint32_t width, uint32_t height, uint32_t rank, uint32_t nranks, uint32_t* out, uint32_t cap,
-                          uint32_t* n_out) {
-    if (!n_out || nranks == 0 || rank >= nranks) return omi::global_error(OM_ERR_INVALID, "om_shard_pixels: bad rank/nranks");
-    if ((uint64_t)width * height > (1ull << 31)) return omi::global_error(OM_ERR_INVALID, "om_shard_pixels: frame too large");
-    std::vector<uint32_t> lst;
-    deal(width, height, rank, nranks, lst);
-    *n_out = (uint32_t)lst.size();
-    if (lst.size() > cap || (!out && !lst.empty()))
-        return omi::global_error(OM_ERR_INVALID, "om_shard_pixels: output too small (see om_shard_capacity)");
-    if (!lst.empty()) std::memcpy(out, lst.data(), lst.size() * 4);
-    return OM_OK;
-}
-
-om_status om_shard_assemble_host(uint32_t width, uint32_t height, uint32_t nranks, const om_pixel_stats* const* shards,
-                                 om_pixel_stats* frame) {
-    if (!shards || !frame || nranks == 0) return omi::global_error(OM_ERR_INVALID, "om_shard_assemble_host: null argument");
-    std::vector<uint32_t> lst;
-    for (uint32_t r = 0; r < nranks; ++r) {
-        deal(width, height, r, nranks, lst);
-        if (!lst.empty() && !shards[r]) return omi::global_error(OM_ERR_INVALID, "om_shard_assemble_host: null shard");
-        for (size_t k = 0; k < lst.size(); ++k) frame[lst[k]] = shards[r][k];
-    }
-    return OM_OK;
-}
 
 om_status om_comm_unique_id(uint8_t id[OM_COMM_ID_BYTES]) {
     static_assert(sizeof(ncclUniqueId) == OM_COMM_ID_BYTES, "ncclUniqueId size");
@@ -307,6 +263,7 @@ struct om_multi {
     std::vector<DBuf> shard;            // per rank: its shard on its device (HBM-resident)
     std::vector<DBuf> staging;          // per rank r > 0: its shard's image on devices[0]
     std::vector<hipEvent_t> ev;         // [0] on devices[0]: frame cut; [r]: rank r done
+    DBuf host_frame;                    // om_multi_render_host: the frame on devices[0]
     std::string err;
 };
 
@@ -390,6 +347,7 @@ void om_multi_destroy(om_multi* m) {
     for (auto& b : m->shard) b.release();
     for (auto& b : m->staging) b.release();
     m->deal.all.release();
+    m->host_frame.release();
     for (size_t r = 0; r < m->ev.size(); ++r)
         if (m->ev[r]) { (void)hipSetDevice(m->dev[r]); (void)hipEventDestroy(m->ev[r]); }
     for (auto c : m->ctx) om_destroy(c);
@@ -483,6 +441,37 @@ om_status om_multi_render(om_multi* m, const om_camera* cam, const om_render_par
     OM_MHIP(m, hipSetDevice(m->dev[0]));
     for (uint32_t r = 0; r < N; ++r)
         OM_MHIP(m, launch_move(true, r ? m->staging[r].p : m->shard[0].p, D.list(r), D.count[r], dev_frame, st[0]));
+    return OM_OK;
+}
+
+om_status om_multi_render_host(om_multi* m, const om_camera* cam, const om_render_params* p, om_pixel_stats* stats,
+                               om_counters* counters) {
+    if (!m || !cam || !p || !stats) return merr(m, OM_ERR_INVALID, "om_multi_render_host: null argument");
+    if (p->width == 0 || p->height == 0 || (uint64_t)p->width * p->height > (1ull << 31))
+        return merr(m, OM_ERR_INVALID, "om_multi_render_host: width/height must be > 0");
+    const size_t bytes = (size_t)p->width * p->height * sizeof(om_pixel_stats);
+    OM_MHIP(m, m->host_frame.ensure(m->dev[0], bytes));
+    hipStream_t st = omi::ctx_stream(m->ctx[0]);
+    for (auto c : m->ctx) {
+        const om_status s = om_reset_counters(c, nullptr);
+        if (s != OM_OK) return merr(m, s, om_last_error(c));
+    }
+    OM_MHIP(m, hipSetDevice(m->dev[0]));
+    OM_MHIP(m, hipMemcpyAsync(m->host_frame.p, stats, bytes, hipMemcpyHostToDevice, st));
+    om_status s = om_multi_render(m, cam, p, (om_pixel_stats*)m->host_frame.p, st);
+    if (s != OM_OK) return s;
+    OM_MHIP(m, hipSetDevice(m->dev[0]));
+    OM_MHIP(m, hipMemcpyAsync(stats, m->host_frame.p, bytes, hipMemcpyDeviceToHost, st));
+    OM_MHIP(m, hipStreamSynchronize(st));
+    if (counters) {
+        *counters = om_counters{};
+        for (auto c : m->ctx) {
+            om_counters k{};
+            if ((s = om_get_counters(c, &k)) != OM_OK) return merr(m, s, om_last_error(c));
+            counters->samples += k.samples; counters->segments += k.segments; counters->prim_tests += k.prim_tests;
+            counters->pre_tests += k.pre_tests; counters->march_steps += k.march_steps; counters->credited += k.credited;
+        }
+    }
     return OM_OK;
 }
 

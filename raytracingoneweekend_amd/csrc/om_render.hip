@@ -209,10 +209,8 @@ __global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(O
         seg++;
         if (finished) {
             const bool done = stats_add(st, result, rdepth, S.bloom[rid]);
-            if (COUNT) {
-                n_samples++;
-                credited += ((done && P.adaptive) ? (P.spp_total - st.n) : 0u) + 1u; // :196-198
-            }
+            if (COUNT) n_samples++;
+            credited += ((done && P.adaptive) ? (P.spp_total - st.n) : 0u) + 1u;     // :196-198
             live = false;
         }
     }
@@ -236,6 +234,10 @@ __global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(O
             atomicAdd(&counters[OMC_MARCH], (unsigned long long)c4);
             atomicAdd(&counters[OMC_CREDITED], (unsigned long long)c5);
         }
+    }
+    if (P.progress) {                                                          // live samples_atom (om_progress)
+        const uint32_t c = wave_sum(credited);
+        if ((threadIdx.x & 63u) == 0u && c) atomicAdd(&counters[OMC_PROGRESS], (unsigned long long)c);
     }
 }
 
@@ -283,6 +285,7 @@ struct om_ctx {
     double tiles_avg = 0.0;
     omw::Timer timer;
     omw::Buffers wf;
+    unsigned long long* progress_host = nullptr;   // om_progress: pinned host word (null: progress off)
     DevBuf frame_list;                  // tile-ordered pixel list of the full frame (wavefront path)
     uint32_t frame_w = 0, frame_h = 0;
     ~om_ctx() {
@@ -292,6 +295,7 @@ struct om_ctx {
         view_scratch.release(); view_rgb.release(); tile_off.release(); tile_idx.release();
         wf.release();
         timer.release();
+        if (progress_host) (void)hipHostFree(progress_host);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -438,9 +442,9 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     om_status s = prepare_jitter(c, p->seed, p->spp_total, &jitter);
     if (s) return s;
     if (!c->counters.p) {
-        s = ensure(c, c->counters, OMC_N * sizeof(unsigned long long));
+        s = ensure(c, c->counters, OMC_SLOTS * sizeof(unsigned long long));
         if (s) return s;
-        OM_HIP(c, hipMemsetAsync(c->counters.p, 0, OMC_N * sizeof(unsigned long long), stream));
+        OM_HIP(c, hipMemsetAsync(c->counters.p, 0, OMC_SLOTS * sizeof(unsigned long long), stream));
     }
     c->last_stream = stream;
     OmCamDev C;
@@ -461,6 +465,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
     P.skey = z ^ (z >> 31);
     P.tiles_x = (p->width + 7u) / 8u;
+    P.progress = c->progress_host ? 1u : 0u;
     uint64_t threads;
     if (dev_pixels) {
         P.n_pixels = n_pixels;
@@ -493,6 +498,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         L.streams = c->wf_streams;
         L.timer = &c->timer;
         L.tile_off = nullptr; L.tile_idx = nullptr;
+        L.progress_host = c->progress_host;
         if (mode == OM_KERNEL_BVH2 && c->scene.n_b2nodes) {
             if ((s = ensure_tile_lists(c, cam, p->width, p->height, stream)) != OM_OK) return s;
             if (c->tiles_use) { L.tile_off = (const uint32_t*)c->tile_off.p; L.tile_idx = (const uint16_t*)c->tile_idx.p; }
@@ -546,6 +552,8 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     }
     c->timer.end(mk_ti, OM_KT_MEGAKERNEL, stream);
     OM_HIP(c, hipGetLastError());
+    if (c->progress_host)   // one launch per call: the word advances when it ends
+        OM_HIP(c, hipMemcpyAsync(c->progress_host, ctr + OMC_PROGRESS, sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     return OM_OK;
 }
 
@@ -684,6 +692,20 @@ om_status om_render(om_ctx* c, const om_camera* cam, const om_render_params* p, 
     return OM_OK;
 }
 
+om_status om_host_register(void* p, size_t bytes) {
+    if (!p || !bytes) return set_err(nullptr, OM_ERR_INVALID, "om_host_register: null/empty buffer");
+    const hipError_t e = hipHostRegister(p, bytes, hipHostRegisterDefault);
+    if (e != hipSuccess) return set_err(nullptr, OM_ERR_DEVICE, std::string("om_host_register: ") + hipGetErrorString(e));
+    return OM_OK;
+}
+
+om_status om_host_unregister(void* p) {
+    if (!p) return set_err(nullptr, OM_ERR_INVALID, "om_host_unregister: null buffer");
+    const hipError_t e = hipHostUnregister(p);
+    if (e != hipSuccess) return set_err(nullptr, OM_ERR_DEVICE, std::string("om_host_unregister: ") + hipGetErrorString(e));
+    return OM_OK;
+}
+
 om_status om_get_counters(om_ctx* c, om_counters* out) {
     if (!c || !out) return set_err(c, OM_ERR_INVALID, "null pointer");
     std::memset(out, 0, sizeof(*out));
@@ -792,6 +814,43 @@ om_status om_display(om_ctx* c, const om_pixel_stats* stats, uint32_t width, uin
     return OM_OK;
 }
 
+const volatile uint64_t* om_progress(om_ctx* c) {
+    if (!c) { set_err(nullptr, OM_ERR_INVALID, "om_progress: null ctx"); return nullptr; }
+    if (c->progress_host) return (const volatile uint64_t*)c->progress_host;
+    if (hipSetDevice(c->device) != hipSuccess) { set_err(c, OM_ERR_DEVICE, "om_progress: hipSetDevice"); return nullptr; }
+    if (!c->counters.p) {
+        if (ensure(c, c->counters, OMC_SLOTS * sizeof(unsigned long long)) != OM_OK) return nullptr;
+        if (hipMemset(c->counters.p, 0, OMC_SLOTS * sizeof(unsigned long long)) != hipSuccess) {
+            set_err(c, OM_ERR_DEVICE, "om_progress: hipMemset");
+            return nullptr;
+        }
+    }
+    unsigned long long* h = nullptr;
+    if (hipHostMalloc((void**)&h, sizeof(unsigned long long), hipHostMallocDefault) != hipSuccess) {
+        set_err(c, OM_ERR_NOMEM, "om_progress: hipHostMalloc");
+        return nullptr;
+    }
+    *h = 0;
+    if (hipStreamSynchronize(c->stream) != hipSuccess ||
+        hipMemcpy(h, (unsigned long long*)c->counters.p + OMC_PROGRESS, sizeof(*h), hipMemcpyDeviceToHost) != hipSuccess) {
+        (void)hipHostFree(h);
+        set_err(c, OM_ERR_DEVICE, "om_progress: reading the device word");
+        return nullptr;
+    }
+    c->progress_host = h;
+    return (const volatile uint64_t*)h;
+}
+
+om_status om_reset_progress(om_ctx* c) {
+    if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
+    if (!c->progress_host) return OM_OK;
+    OM_HIP(c, hipSetDevice(c->device));
+    OM_HIP(c, hipDeviceSynchronize());
+    OM_HIP(c, hipMemset((unsigned long long*)c->counters.p + OMC_PROGRESS, 0, sizeof(unsigned long long)));
+    *(volatile unsigned long long*)c->progress_host = 0;
+    return OM_OK;
+}
+
 om_status om_set_counting(om_ctx* c, int32_t enable) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
     c->count_work = enable != 0;
@@ -801,9 +860,12 @@ om_status om_set_counting(om_ctx* c, int32_t enable) {
 om_status om_reset_counters(om_ctx* c, void* stream) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
     OM_HIP(c, hipSetDevice(c->device));
-    om_status s = ensure(c, c->counters, OMC_N * sizeof(unsigned long long));
+    const bool fresh = !c->counters.p;
+    om_status s = ensure(c, c->counters, OMC_SLOTS * sizeof(unsigned long long));
     if (s) return s;
-    OM_HIP(c, hipMemsetAsync(c->counters.p, 0, OMC_N * sizeof(unsigned long long), stream ? (hipStream_t)stream : c->stream));
+    // the counters only; the progress word after them keeps counting (om_reset_progress)
+    OM_HIP(c, hipMemsetAsync(c->counters.p, 0, (fresh ? OMC_SLOTS : OMC_N) * sizeof(unsigned long long),
+                             stream ? (hipStream_t)stream : c->stream));
     return OM_OK;
 }
 

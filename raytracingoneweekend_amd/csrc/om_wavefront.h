@@ -88,6 +88,7 @@ struct Launch {
     Timer* timer;                // per-launch event timing (may be off)
     const uint32_t* tile_off;    // primary-ray candidate lists per 8x8 tile (null = traverse the BVH)
     const uint16_t* tile_idx;
+    unsigned long long* progress_host;   // om_progress word (pinned host) or null; device side counters[OMC_PROGRESS]
 };
 
 // Renders P.sample_count samples of every listed pixel; returns 0 or a HIP error text.

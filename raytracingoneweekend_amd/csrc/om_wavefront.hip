@@ -668,10 +668,8 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
             if (id == kNoSample) continue;
             const float4 rr = res[t];
             const bool done = stats_add(st, f3(rr.x, rr.y, rr.z), rr.w, bloom[id]);
-            if (COUNT) {
-                n_samples++;
-                credited += ((done && P.adaptive) ? (P.spp_total - st.n) : 0u) + 1u;   // render_thread.rs:196-198
-            }
+            if (COUNT) n_samples++;
+            credited += ((done && P.adaptive) ? (P.spp_total - st.n) : 0u) + 1u;   // render_thread.rs:196-198
         }
         om_pixel_stats out;
         out.bloom = st.bloom; out.sum[0] = st.sx; out.sum[1] = st.sy; out.sum[2] = st.sz; out.n = st.n;
@@ -684,6 +682,7 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
         flush_counter(counters, OMC_SAMPLES, n_samples);
         flush_counter(counters, OMC_CREDITED, credited);
     }
+    if (P.progress) flush_counter(counters, OMC_PROGRESS, credited);      // live samples_atom (om_progress)
 }
 
 // k_snapshot: n0[k] = Stats.n of listed pixel k at the start of a fixed-spp call.
@@ -921,6 +920,12 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
             hipLaunchKernelGGL(k_accumulate<false>, dim3(grid_a), dim3(kBlk), 0, si, L.P, L.stats, L.pixels, n_px,
                                L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, L.counters);
         tm.end(ati, OM_KT_ACCUMULATE, si);
+        // live progress: the cumulative credit after this batch, to the host word om_progress
+        // hands out; ahead of the event the next batch's accumulate waits on, so the copies
+        // land in order and the word only grows
+        if (L.progress_host)
+            (void)hipMemcpyAsync(L.progress_host, L.counters + OMC_PROGRESS, sizeof(unsigned long long),
+                                 hipMemcpyDeviceToHost, si);
         if (ns > 1) (void)hipEventRecord(B.ev[kMaxSets + i], si);
         if ((e = hipGetLastError()) != hipSuccess) { err = "wavefront launch failed"; return e; }
         done += b;

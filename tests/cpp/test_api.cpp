@@ -147,15 +147,37 @@ static int run_gpu(const char* out_fixed, const char* out_adaptive) {
     const Camera cam = default_camera((float)W / (float)H);
     HittableList world = random_scene(0x5EED, false);
     const FrozenHittableList frozen = world.freeze(cam);
+    std::vector<Pixel> fixed(W * H);
     {   // fixed spp (adaptive off), split into progressive calls of 3 samples
-        std::vector<Pixel> px(W * H);
         RenderOptions opt;
         opt.adaptive = false;
         opt.samples_per_call = 3;
         opt.seed = 7;
-        const uint64_t credited = render_threads(cam, frozen, W, H, 8, px, opt, 3);
+        const uint64_t credited = render_threads(cam, frozen, W, H, 8, fixed, opt, 3);
         EXPECT(credited == (uint64_t)W * H * 8);
-        write_raw(out_fixed, px);
+        write_raw(out_fixed, fixed);
+    }
+    {   // the default: one call for the frame, samples_atom fed by the live progress word
+        std::vector<Pixel> px(W * H);
+        RenderOptions opt;
+        opt.adaptive = false;
+        opt.seed = 7;
+        const uint64_t credited = render_threads(cam, frozen, W, H, 8, px, opt, 2);
+        EXPECT(credited == (uint64_t)W * H * 8);
+        EXPECT(std::memcmp(px.data(), fixed.data(), px.size() * sizeof(Pixel)) == 0);
+    }
+    {   // the frame over 3 logical ranks on device 0 (MultiFrame: tile shards + gather)
+        MultiFrame multi(world, {0, 0, 0});
+        EXPECT(multi.transport() == OM_TRANSPORT_LOCAL);
+        std::vector<Pixel> px(W * H);
+        std::atomic<uint64_t> atom{0};
+        RenderOptions opt;
+        opt.adaptive = false;
+        opt.seed = 7;
+        opt.samples_per_call = 5;
+        multi.render(cam, 50, 0.001f, 100.0f, 8, W, H, PixelsBox{&px}, atom, opt);
+        EXPECT(atom.load() == (uint64_t)W * H * 8);
+        EXPECT(std::memcmp(px.data(), fixed.data(), px.size() * sizeof(Pixel)) == 0);
     }
     {   // the reference's default: adaptive retirement, credits = every sample of the frame
         std::vector<Pixel> px(W * H);

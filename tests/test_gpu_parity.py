@@ -406,3 +406,37 @@ def test_python_render_defaults_to_reference_adaptive(om, oracle):
     assert nb == 0, msg
     assert pix.pixels["n"].min() < SPP
     assert atom[0] == W * H * SPP
+
+
+@pytest.mark.parametrize("pipeline,adaptive", [("wavefront", False), ("wavefront", True), ("megakernel", False)])
+def test_live_progress_word(om, pipeline, adaptive):
+    """om_progress: the samples_atom word (render_thread.rs:196-198) advances while a call runs
+    (the wavefront adds each accumulated batch) and ends equal to the call's credited count."""
+    import ctypes as C
+    import torch
+    from raytracingoneweekend_amd import _lib as L
+    W, H, SPP = (1920, 1080, 64) if not adaptive else (640, 360, 96)
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam, pipeline=pipeline)
+    prog = L.lib.om_progress(fz.ctx)
+    assert prog and prog[0] == 0
+    frame = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.Stream()
+    torch.cuda.synchronize()
+    L.check(L.lib.om_reset_counters(fz.ctx, C.c_void_p(s.cuda_stream)), fz.ctx)
+    p = om.make_params(50, 0.001, 100.0, SPP, W, H, seed=3, adaptive=adaptive)
+    L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(frame.data_ptr()),
+                                   C.c_void_p(s.cuda_stream)), fz.ctx)
+    seen = []
+    while not s.query():
+        seen.append(int(prog[0]))
+    s.synchronize()
+    seen.append(int(prog[0]))
+    ctr = fz.counters()
+    assert all(a <= b for a, b in zip(seen, seen[1:])), "progress went backwards"
+    assert seen[-1] == ctr["credited"] == W * H * SPP
+    if pipeline == "wavefront":
+        assert any(0 < v < seen[-1] for v in seen), "no progress seen inside the call"
+    L.check(L.lib.om_reset_progress(fz.ctx), fz.ctx)
+    assert prog[0] == 0

@@ -1,6 +1,8 @@
 """Secondary measurements for DESIGN.md (GPU box):
   * C1 through the HOST framebuffer entry point om_render (stats copied host -> device ->
-    host every call: the PCIe-inclusive rate; bench.py's `value` keeps stats in HBM);
+    host every call: the PCIe-inclusive rate; bench.py's `value` keeps stats in HBM), with
+    the framebuffer page-locked (PixelsBox, om_host_register) or pageable, at 512 / 32 / 16
+    spp per call, beside the device-resident rate of the same frame;
   * C0, the reference's own CPU case (400x225, 64 spp, depth 8): GPU (om_render_device)
     and the CPU oracle on this host's cores (the reference's num_cpus-1 thread scheme).
 One JSON line.  python tools/host_path.py
@@ -21,22 +23,56 @@ import raytracingoneweekend_amd as om  # noqa: E402
 from raytracingoneweekend_amd import _lib as L  # noqa: E402
 
 
-def main():
-    out = {}
-    # ---- C1 host path: 4 calls of 16 spp through om_render (host stats, includes PCIe)
+def c1_host(per_call, pinned, spp=512):
+    """C1 through om_render (host Stats: the PCIe-inclusive rate), `per_call` spp per call."""
     W, H = 1920, 1080
     cam = om.default_camera(W / H)
     fz = om.random_scene(0x5EED).freeze(cam)
-    pix = om.PixelsBox.new(W * H)
-    om.render(cam, fz, 50, 0.001, 100.0, 64, W, H, pix, seed=1, sample_count=16, adaptive=False)          # warm-up
-    pix = om.PixelsBox.new(W * H)
+    L.check(L.lib.om_set_counting(fz.ctx, 0), fz.ctx)
+    box = om.PixelsBox.new(W * H)
+    target = box if pinned else box.pixels                   # a bare array stays pageable
+    om.render(cam, fz, 50, 0.001, 100.0, spp, W, H, target, seed=1, sample_count=per_call, adaptive=False)  # warm-up
+    box.pixels[:] = 0
     t0 = time.perf_counter()
-    for _ in range(4):
-        om.render(cam, fz, 50, 0.001, 100.0, 64, W, H, pix, seed=1, sample_count=16, adaptive=False)
+    for _ in range(spp // per_call):
+        om.render(cam, fz, 50, 0.001, 100.0, spp, W, H, target, seed=1, sample_count=per_call, adaptive=False)
     dt = time.perf_counter() - t0
-    assert int(pix.pixels["n"].min()) == 64
-    out["c1_host_path"] = {"msamples_s": round(W * H * 64 / dt / 1e6, 1), "calls": 4, "spp_per_call": 16,
-                           "stats_bytes_each_way": W * H * 40}
+    assert int(box.pixels["n"].min()) == spp
+    return {"msamples_s": round(W * H * spp / dt / 1e6, 1), "calls": spp // per_call, "spp_per_call": per_call,
+            "pinned": pinned, "stats_bytes_each_way_per_call": W * H * 40}
+
+
+def c1_device(per_call=32, spp=512):
+    """The same frame with device-resident Stats (om_render_device): bench.py's value."""
+    W, H = 1920, 1080
+    cam = om.default_camera(W / H)
+    fz = om.random_scene(0x5EED).freeze(cam)
+    L.check(L.lib.om_set_counting(fz.ctx, 0), fz.ctx)
+    st = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.Stream()
+    p = om.make_params(50, 0.001, 100.0, spp, W, H, sample_count=per_call, seed=1)
+    go = lambda: L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()),
+                                                C.c_void_p(s.cuda_stream)), fz.ctx)
+    go()
+    torch.cuda.synchronize()
+    st.zero_()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(spp // per_call):
+        go()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    return {"msamples_s": round(W * H * spp / dt / 1e6, 1), "calls": spp // per_call, "spp_per_call": per_call}
+
+
+def main():
+    out = {}
+    dev = c1_device()
+    out["c1_device_resident"] = dev
+    for per_call, pinned in ((512, True), (32, True), (32, False), (16, True)):
+        r = c1_host(per_call, pinned)
+        r["of_device_resident"] = round(r["msamples_s"] / dev["msamples_s"], 3)
+        out[f"c1_host_{per_call}spp_{'pinned' if pinned else 'pageable'}"] = r
     # ---- C0 on the GPU (device stats) and on the CPU oracle
     W0, H0, SPP0, D0 = 400, 225, 64, 8
     cam0 = om.default_camera(W0 / H0)
