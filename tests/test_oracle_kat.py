@@ -263,3 +263,74 @@ def test_adaptive_credit(oracle):
     # constant sky: colour fixed after sample 1 -> 5 bad runs -> retire at n = 6 (render_thread.rs:31-38)
     assert (st["n"] == 6).all()
     assert ctr["credited"] == 4 * 20                                 # skipped samples credited (:196-198)
+
+
+# ---- reference-semantics traps: each pins one place where the reference
+# departs from the textbook integrator, so the oracle cannot silently "fix" it
+
+def test_metal_never_absorbs_below_surface(oracle):
+    """materials.rs:62-66: Metal::scatter always returns the fuzzed reflection, even when it
+    points into the surface (the textbook version absorbs when scattered . n <= 0)."""
+    mat = oracle.material("metal", (0.9, 0.8, 0.7), fuzz=1.0)
+    d = np.array([1.0, -0.05, 0.0], dtype=F)
+    d = d / np.linalg.norm(d)
+    below = 0
+    for st in range(200):
+        r = _scatter(oracle, (0, 0, 0, *d), (1, 0, 0, 0, 0, 1, 0), mat, st)
+        assert np.allclose(r[0:3], [0.9, 0.8, 0.7])                     # attenuation = albedo, always
+        assert abs(np.linalg.norm(r[6:9]) - 1) < 1e-5                  # Ray::new normalises (ray.rs:12)
+        below += r[7] < 0
+    assert below > 0                                                   # some rays go into the surface
+
+
+def test_ellipsoid_normal_is_l2w_of_local_point(oracle):
+    """traced.rs:59: normal = unit(L2W . p_local), not the inverse-transpose (geometric) normal."""
+    w = oracle.World()
+    w.add_sphere(np.diag([2., 1., 1., 1.]).astype(F), _lam(oracle))
+    out, _ = w.hit((-10., 0.5, 0.), (1., 0., 0.))
+    lp = np.array([-np.sqrt(F(0.75)), 0.5, 0.0], dtype=F)               # local hit point on the unit sphere
+    ref = np.array([2.0, 1.0, 1.0], dtype=F) * lp
+    ref = ref / np.linalg.norm(ref)                                    # (-0.961, 0.277, 0)
+    geo = lp / np.array([2.0, 1.0, 1.0], dtype=F)
+    geo = geo / np.linalg.norm(geo)                                    # (-0.655, 0.756, 0): NOT what the reference does
+    assert np.allclose(out[4:7], ref, atol=1e-6)
+    assert not np.allclose(out[4:7], geo, atol=1e-2)
+
+
+def test_cube_normal_is_not_normalised(oracle):
+    """traced.rs:296: Cube's normal is L2W . (axis * sign) without .unit()."""
+    w = oracle.World()
+    w.add_cube(np.diag([1., 3., 1., 1.]).astype(F), _lam(oracle))      # unit cube stretched 3x in y
+    out, _ = w.hit((0., 10., 0.), (0., -1., 0.))
+    assert out[0] == F(10.0 - 1.5)
+    assert tuple(out[4:7]) == (0., 3., 0.)                             # length 3
+
+
+def test_refract_takes_abs_before_sqrt(oracle):
+    """materials.rs:105: r_out_parallel = -sqrt(|1 - |perp|^2|) n.  With the cube's unnormalised
+    normal (length 3) |perp|^2 > 1 although cannot_refract is false (cos_theta clamps to 1):
+    the abs keeps the refracted direction finite where the textbook form gives NaN."""
+    mat = oracle.material("dielectric", ior=1.5)
+    s = F(1.0) / np.sqrt(F(2.0))
+    st = next(k for k in range(2000) if _path_state_draws_py(k, 1)[0] > 0.04)   # refract, not Schlick-reflect
+    r = _scatter(oracle, (0, 0, 0, s, -s, 0), (1, 0, 0, 0, 0, 3, 0), mat, st)
+    n = np.array([0, 3, 0], dtype=F)
+    uv = np.array([s, -s, 0], dtype=F)
+    ratio = F(1.0) / F(1.5)
+    perp = ratio * (uv + F(1.0) * n)
+    assert float(perp @ perp) > 1.0
+    out = perp + (-np.sqrt(np.abs(F(1.0) - perp @ perp))) * n
+    assert np.all(np.isfinite(r[6:9]))
+    assert np.allclose(r[6:9], out / np.linalg.norm(out), atol=1e-6)
+
+
+def test_exhausted_depth_colour_is_negative_zero(oracle):
+    """render_thread.rs:142: a path that runs out of depth returns -Color::ZERO; Stats::add of
+    it onto Color::ZERO gives +0 sums (IEEE: +0 + -0 = +0), so the frame shows black with
+    n counted and the first hit's depth, never a NaN (checked bit for bit)."""
+    w = oracle.World()
+    w.add_sphere_radius((0., 0., 0.), 10., oracle.material("metal", (1., 1., 1.)))
+    cam = oracle.camera((0., 0., 0.), (0., 0., -1.), (0., 1., 0.), 40., 1., 0., 1.)
+    st, _ = _render_one(oracle, w, cam, depth=3)
+    assert (st["sum"].view(np.uint32) == 0).all()                      # +0 bit patterns
+    assert (st["color"] == 0).all() and (st["n"] == 2).all()
