@@ -76,6 +76,9 @@ __device__ __forceinline__ F3 rand_in_unit_sphere(Rng& g) {                     
 }
 
 // ---------------------------------------------------------------- traced.rs
+#ifndef OM_SPHERE_FAST_REJECT
+#define OM_SPHERE_FAST_REJECT 1
+#endif
 // Sphere::hit (traced.rs:39-62) up to the accepted root.
 __device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root) {
     const F3 lo = xform_p(T.w2l, o);
@@ -86,9 +89,23 @@ __device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, f
     const float disc = half_b * half_b - a * c;
     if (disc < 0.0f) return false;
     const float sqrtd = sqrtf(disc);
-    float r = (-half_b - sqrtd) / a;
+    const float n1 = -half_b - sqrtd, n2 = -half_b + sqrtd;
+#if OM_SPHERE_FAST_REJECT
+    // Both roots provably outside [tmin, tmax] without the two correctly rounded divisions
+    // (~24 VALU): for a > 0 in the normal range, n < (tmin*a)(1-2^-18) implies
+    // fl(n/a) < tmin and n > (tmax*a)(1+2^-18) implies fl(n/a) > tmax, whatever the f32
+    // rounding of the products and of the quotient (each within 2^-24 relative), and
+    // r1 <= r2 because n1 <= n2.  Only rejections the reference makes are skipped (a ray
+    // leaving the surface it just hit, the ground sphere behind the current hit ...);
+    // NaNs fail every compare and take the exact path.
+    if (a >= 1e-30f && a <= 1e30f) {
+        const float lo = (tmin * a) * (1.0f - 0x1p-18f), hi = (tmax * a) * (1.0f + 0x1p-18f);
+        if (n2 < lo || n1 > hi || (n1 < lo && n2 > hi)) return false;
+    }
+#endif
+    float r = n1 / a;
     if (r < tmin || r > tmax) {
-        r = (-half_b + sqrtd) / a;
+        r = n2 / a;
         if (r < tmin || r > tmax) return false;
     }
     root = r;

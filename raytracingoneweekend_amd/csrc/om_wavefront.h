@@ -34,6 +34,7 @@ struct Buffers {
     uint32_t* n0 = nullptr;      // per listed pixel: Stats.n at the start of the call
     uint64_t n0_cap = 0;
     hipStream_t side[kMaxSets] = {};  // streams 1.. of the overlapped schedule
+    hipStream_t tail[2] = {};         // async tails: batch i's tail + accumulate run on tail[i % 2]
     std::vector<hipEvent_t> ev;  // cross-stream ordering events (timing disabled)
     void release();
 };

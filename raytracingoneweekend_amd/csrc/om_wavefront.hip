@@ -49,6 +49,7 @@ void Buffers::release() {
     if (n0) (void)hipFree(n0);
     n0 = nullptr; n0_cap = 0;
     for (auto& st : side) { if (st) (void)hipStreamDestroy(st); st = nullptr; }
+    for (auto& st : tail) { if (st) (void)hipStreamDestroy(st); st = nullptr; }
     for (auto e : ev) (void)hipEventDestroy(e);
     ev.clear();
     cap = 0; counts_n = 0; nsets = 0;
@@ -87,6 +88,21 @@ __host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
 #define OM_WF_TAIL_SPB 2
 #endif
 constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segments per tail workgroup
+// Async tails (OM_WF_ASYNC_TAIL, fixed-spp calls): each batch's tail runs on the context's tail
+// stream while its main stream already starts the call's next batch on another queue set, so
+// the latency-bound tails (a chain of up to max_depth - T serial bounces of the longest paths)
+// overlap the heavy early bounces instead of leaving the chip idle at every batch boundary.
+// The tail grid is narrow (kTailSpbAsync segments per workgroup) so it holds few CU slots.
+#ifndef OM_WF_ASYNC_TAIL
+#define OM_WF_ASYNC_TAIL 0
+#endif
+#ifndef OM_WF_TAIL_SPB_ASYNC
+#define OM_WF_TAIL_SPB_ASYNC 2
+#endif
+#ifndef OM_WF_TAIL_PRIO
+#define OM_WF_TAIL_PRIO 1
+#endif
+constexpr uint32_t kTailSpbAsync = OM_WF_TAIL_SPB_ASYNC;
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
 // Work distribution inside a bounce workgroup.  1 (default): every wave takes 64-path
 // chunks of the segment from an LDS counter and appends its survivors with one LDS atomic,
@@ -597,24 +613,24 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_march(OmSceneDev S, OmPa
 // ---------------------------------------------------------------- tail
 // Workgroup b: every path of segments [b*kTailSpb, (b+1)*kTailSpb) of queue `in`, each
 // run to completion; a lane whose path ends takes the next one from an LDS counter.
-template <int TR, bool COUNT, bool MARCH>
+template <int TR, bool COUNT, bool MARCH, uint32_t SPB = kTailSpb>
 __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
                                                const uint32_t* __restrict__ count_in, float4* __restrict__ res,
                                                uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters) {
-    __shared__ uint32_t pre[kTailSpb + 1];
+    __shared__ uint32_t pre[SPB + 1];
     __shared__ uint32_t next;
-    const uint32_t s0 = blockIdx.x * kTailSpb;
+    const uint32_t s0 = blockIdx.x * SPB;
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
-        for (uint32_t k = 0; k < kTailSpb; ++k) {
+        for (uint32_t k = 0; k < SPB; ++k) {
             pre[k] = acc;
             acc += s0 + k < G.nseg ? count_in[s0 + k] : 0u;
         }
-        pre[kTailSpb] = acc;
+        pre[SPB] = acc;
         next = kBlk;
     }
     __syncthreads();
-    const uint32_t total = pre[kTailSpb];
+    const uint32_t total = pre[SPB];
     if (total == 0) return;
     const Tracer T = stage_scene<TR>(S);
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
@@ -725,9 +741,37 @@ Queue queue(QueueSet& B, int k) { return Queue{B.q[k][0], B.q[k][1], B.q[k][2], 
 
 // One batch: bounce 0 .. tail_at-1 as per-bounce launches, then the tail launch; returns
 // the number of bounce-family launches.
+// Async tails (Tail.ev set): the bounce launches go on `st`; the event is recorded after the
+// last of them, and the tail launch (narrow: kTailSpbAsync segments per workgroup, so it holds
+// few CU slots while it trickles) goes on Tail.st behind it.  Otherwise the tail follows on st.
+struct Tail {
+    hipStream_t st;
+    hipEvent_t ev;
+};
+template <int TR, bool COUNT, bool MARCH>
+__host__ inline void launch_tail(const Launch& L, QueueSet& B, Seg G, const Queue& in, const uint32_t* cin, uint32_t lds,
+                                 hipStream_t st, const Tail& T, Timer& tm, bool each) {
+    hipStream_t ts = st;
+    if (T.ev) {
+        (void)hipEventRecord(T.ev, st);
+        (void)hipStreamWaitEvent(T.st, T.ev, 0);
+        ts = T.st;
+    }
+    const int ti = each ? tm.begin(ts) : -1;
+    if (T.ev) {
+        const uint32_t grid = (G.nseg + kTailSpbAsync - 1u) / kTailSpbAsync;
+        hipLaunchKernelGGL((k_tail<TR, COUNT, MARCH, kTailSpbAsync>), dim3(grid), dim3(kBlk), lds, ts, L.S, L.P, G, in, cin,
+                           B.res, B.res_id, L.counters);
+    } else {
+        const uint32_t grid = (G.nseg + kTailSpb - 1u) / kTailSpb;
+        hipLaunchKernelGGL((k_tail<TR, COUNT, MARCH>), dim3(grid), dim3(kBlk), lds, ts, L.S, L.P, G, in, cin,
+                           B.res, B.res_id, L.counters);
+    }
+    tm.end(ti, OM_KT_TAIL, ts);
+}
 template <int TR, bool COUNT, bool MARCH>
 uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Gen& R, uint32_t depth_cap,
-                   uint32_t tail_at, uint32_t lds) {
+                   uint32_t tail_at, uint32_t lds, const Tail& T) {
     Timer& tm = *L.timer;
     const bool each = tm.mode == 1;
     uint32_t launches = 0;
@@ -742,11 +786,7 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
             const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
             const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
             if (bounce > 0 && bounce >= tail_at) {
-                const uint32_t grid = (G.nseg + kTailSpb - 1u) / kTailSpb;
-                const int ti = each ? tm.begin(st) : -1;
-                hipLaunchKernelGGL((k_tail<TR, COUNT, MARCH>), dim3(grid), dim3(kBlk), lds, st, L.S, L.P, G, in, cin,
-                                   B.res, B.res_id, L.counters);
-                tm.end(ti, OM_KT_TAIL, st);
+                launch_tail<TR, COUNT, MARCH>(L, B, G, in, cin, lds, st, T, tm, each);
                 return launches + 1u;
             }
             uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
@@ -765,17 +805,14 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
             tm.end(ti, kc, st);
             launches += 2u;
         }
+        if (T.ev) { (void)hipEventRecord(T.ev, st); (void)hipStreamWaitEvent(T.st, T.ev, 0); }
         return launches;
     }
     for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
         const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
         const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
         if (bounce > 0 && bounce >= tail_at) {
-            const uint32_t grid = (G.nseg + kTailSpb - 1u) / kTailSpb;
-            const int ti = each ? tm.begin(st) : -1;
-            hipLaunchKernelGGL((k_tail<TR, COUNT, MARCH>), dim3(grid), dim3(kBlk), lds, st, L.S, L.P, G, in, cin,
-                               B.res, B.res_id, L.counters);
-            tm.end(ti, OM_KT_TAIL, st);
+            launch_tail<TR, COUNT, MARCH>(L, B, G, in, cin, lds, st, T, tm, each);
             return launches + 1u;
         }
         uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
@@ -789,16 +826,17 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         tm.end(ti, bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE, st);
         ++launches;
     }
+    if (T.ev) { (void)hipEventRecord(T.ev, st); (void)hipStreamWaitEvent(T.st, T.ev, 0); }
     return launches;
 }
 
 template <int TR>
 uint32_t run_tr(bool count, bool march, QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Gen& R,
-                uint32_t depth_cap, uint32_t tail_at, uint32_t lds) {
-    if (count && march) return run_batch<TR, true, true>(B, L, st, G, R, depth_cap, tail_at, lds);
-    if (count) return run_batch<TR, true, false>(B, L, st, G, R, depth_cap, tail_at, lds);
-    if (march) return run_batch<TR, false, true>(B, L, st, G, R, depth_cap, tail_at, lds);
-    return run_batch<TR, false, false>(B, L, st, G, R, depth_cap, tail_at, lds);
+                uint32_t depth_cap, uint32_t tail_at, uint32_t lds, const Tail& T) {
+    if (count && march) return run_batch<TR, true, true>(B, L, st, G, R, depth_cap, tail_at, lds, T);
+    if (count) return run_batch<TR, true, false>(B, L, st, G, R, depth_cap, tail_at, lds, T);
+    if (march) return run_batch<TR, false, true>(B, L, st, G, R, depth_cap, tail_at, lds, T);
+    return run_batch<TR, false, false>(B, L, st, G, R, depth_cap, tail_at, lds, T);
 }
 
 hipError_t ensure_events(Buffers& B, size_t n) {
@@ -837,6 +875,10 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     if (concurrent) batch = std::min<uint32_t>(batch, (L.P.sample_count + want - 1u) / want);
     const uint32_t nb = (L.P.sample_count + batch - 1u) / batch;
     const uint32_t ns = concurrent ? std::min<uint32_t>(want, nb) : 1u;
+    // async tails (fixed spp, concurrent batches): each main stream alternates between two queue
+    // sets, so a batch's tail and accumulate (on a tail stream) overlap the next batch's bounces
+    const bool async_tail = OM_WF_ASYNC_TAIL && concurrent && ns >= 2u && 2u * ns <= (uint32_t)kMaxSets;
+    const uint32_t nsets = async_tail ? std::min<uint32_t>(2u * ns, nb) : ns;
     const uint32_t depth_cap = L.P.max_depth > 1u ? L.P.max_depth : 1u;
     const uint32_t tail_at = L.tail_bounce ? L.tail_bounce : kTailDefault;
     int dev = 0;
@@ -848,7 +890,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (OM_WF_LANES_PER_CU / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
     const uint32_t segcap = seg_capacity(max_paths, nseg);
-    hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg, (int)ns);
+    hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg, (int)nsets);
     if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
     int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
     if (tr == TR_BVH4_LDS) tr = L.S.n_b4nodes == 0 ? TR_BVH2_LDS : (L.S.b4_lds_bytes ? TR_BVH4_LDS : TR_BVH4_GLOBAL);
@@ -877,9 +919,11 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
                            R.by_pixel, B.n0);
         R.n0 = B.n0;
     }
-    // events: [0] call start on `st`, [k] side stream k joined, [kMaxSets + i] batch i accumulated
+    // events: [0] call start on `st`, [k] side stream k joined (or, async tails: [1], [2] tail
+    // streams done), [kMaxSets + i] batch i accumulated; async tails: [kMaxSets + nb + i] batch
+    // i's bounces launched (its tail waits on it)
     if (ns > 1) {
-        if ((e = ensure_events(B, kMaxSets + nb)) != hipSuccess) { err = "event creation failed"; return e; }
+        if ((e = ensure_events(B, kMaxSets + 2u * nb)) != hipSuccess) { err = "event creation failed"; return e; }
         (void)hipEventRecord(B.ev[0], st);                       // side streams start after everything before the call
         for (uint32_t k = 1; k < ns; ++k) {
             if (!B.side[k] && (e = hipStreamCreateWithFlags(&B.side[k], hipStreamNonBlocking)) != hipSuccess) {
@@ -888,28 +932,46 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
             streams[k] = B.side[k];
             (void)hipStreamWaitEvent(streams[k], B.ev[0], 0);
         }
+        for (uint32_t k = 0; async_tail && k < 2u; ++k) {
+            if (!B.tail[k]) {
+                // high priority: the tail + accumulate chain is latency-bound and gates the reuse of
+                // its queue set; the dispatcher serves its workgroups ahead of the bounce launches'.
+                // Its own HW queue pool also keeps it off the main streams' in-order queues.
+                int lo = 0, hi = 0;
+                (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+                if ((e = hipStreamCreateWithPriority(&B.tail[k], hipStreamNonBlocking, OM_WF_TAIL_PRIO ? hi : lo)) != hipSuccess) {
+                    err = "tail stream creation failed"; return e;
+                }
+            }
+            (void)hipStreamWaitEvent(B.tail[k], B.ev[0], 0);
+        }
     }
     uint32_t launches = 0;
     for (uint32_t i = 0, done = 0; i < nb; ++i) {
         const uint32_t b = std::min(batch, L.P.sample_count - done);
         const uint64_t paths = (uint64_t)n_px * b;
         hipStream_t si = streams[i % ns];
-        QueueSet& QS = B.set[i % ns];
+        QueueSet& QS = B.set[i % nsets];
+        // async tails: batch i's tail + accumulate go on tail stream i % 2, behind its bounces; the
+        // queue set is reused by batch i + nsets only after batch i is accumulated
+        const Tail TT{async_tail ? B.tail[i % 2u] : si, async_tail ? B.ev[kMaxSets + nb + i] : nullptr};
+        if (async_tail && i >= nsets) (void)hipStreamWaitEvent(si, B.ev[kMaxSets + i - nsets], 0);
         Seg G;
         G.nseg = nseg;
         G.segcap = seg_capacity(paths, nseg);
         R.batch = b;
         R.done = done;
         switch (tr) {
-            case TR_BRUTE: launches += run_tr<TR_BRUTE>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
-            case TR_CULLED: launches += run_tr<TR_CULLED>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
-            case TR_BVH: launches += run_tr<TR_BVH>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
-            case TR_SBVH_GLOBAL: launches += run_tr<TR_SBVH_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
-            case TR_BVH2_LDS: launches += run_tr<TR_BVH2_LDS>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
-            case TR_BVH4_LDS: launches += run_tr<TR_BVH4_LDS>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
-            case TR_BVH4_GLOBAL: launches += run_tr<TR_BVH4_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
-            default: launches += run_tr<TR_BVH2_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
+            case TR_BRUTE: launches += run_tr<TR_BRUTE>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
+            case TR_CULLED: launches += run_tr<TR_CULLED>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
+            case TR_BVH: launches += run_tr<TR_BVH>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
+            case TR_SBVH_GLOBAL: launches += run_tr<TR_SBVH_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
+            case TR_BVH2_LDS: launches += run_tr<TR_BVH2_LDS>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
+            case TR_BVH4_LDS: launches += run_tr<TR_BVH4_LDS>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
+            case TR_BVH4_GLOBAL: launches += run_tr<TR_BVH4_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
+            default: launches += run_tr<TR_BVH2_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
         }
+        if (async_tail) si = TT.st;                                  // accumulate behind the tail
         if (ns > 1 && i > 0) (void)hipStreamWaitEvent(si, B.ev[kMaxSets + i - 1u], 0);   // Stats::add in sample order
         const uint32_t grid_a = (n_px + kBlk - 1) / kBlk;
         const int ati = tm.mode == 1 ? tm.begin(si) : -1;
@@ -930,9 +992,20 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
         if ((e = hipGetLastError()) != hipSuccess) { err = "wavefront launch failed"; return e; }
         done += b;
     }
-    for (uint32_t k = 1; k < ns; ++k) {                           // the call ends joined on `st`
-        (void)hipEventRecord(B.ev[k], streams[k]);
-        (void)hipStreamWaitEvent(st, B.ev[k], 0);
+    if (async_tail) {                                             // the call ends joined on `st`: the
+        for (uint32_t k = 0; k < 2u; ++k) {                       // tail streams end every batch (its
+            (void)hipEventRecord(B.ev[1u + k], B.tail[k]);        // accumulate), behind its bounces
+            (void)hipStreamWaitEvent(st, B.ev[1u + k], 0);
+        }
+        for (uint32_t k = 1; k < ns; ++k) {
+            (void)hipEventRecord(B.ev[2u + k], streams[k]);
+            (void)hipStreamWaitEvent(st, B.ev[2u + k], 0);
+        }
+    } else {
+        for (uint32_t k = 1; k < ns; ++k) {
+            (void)hipEventRecord(B.ev[k], streams[k]);
+            (void)hipStreamWaitEvent(st, B.ev[k], 0);
+        }
     }
     tm.end(call_ti, OM_KT_BOUNCE_SPAN, st, launches);
     return hipSuccess;

@@ -9,7 +9,10 @@ driving several GPUs, inside om_multi_render.  Pixels are independent and om-rng
 
 Everything here marshals arguments to libottomarcher.so; nothing is computed in Python.
 """
+import contextlib
 import ctypes as C
+import os
+import sys
 
 import numpy as np
 
@@ -44,6 +47,20 @@ def assemble(width, height, shards):
     return frame
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """RCCL prints a version banner on stdout when a communicator is created; a front-end whose
+    stdout is data (bench.py's one JSON line) keeps it on stderr."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def unique_id():
     """om_comm_unique_id: the 128 bytes rank 0 hands to every rank before Comm()."""
     buf = (C.c_uint8 * L.OM_COMM_ID_BYTES)()
@@ -61,7 +78,8 @@ class Comm:
         self.ctx, self.world_size, self.rank = ctx, int(world_size), int(rank)
         self._c = C.c_void_p()
         idbuf = (C.c_uint8 * L.OM_COMM_ID_BYTES).from_buffer_copy(uid)
-        check(lib.om_comm_init_rank(ctx, self.world_size, self.rank, idbuf, C.byref(self._c)), ctx)
+        with _stdout_to_stderr():
+            check(lib.om_comm_init_rank(ctx, self.world_size, self.rank, idbuf, C.byref(self._c)), ctx)
 
     def render_shard(self, cam, params, dev_shard_ptr, stream=None):
         check(lib.om_render_shard(self._c, C.byref(cam.raw if hasattr(cam, "raw") else cam), C.byref(params),
@@ -91,7 +109,8 @@ class MultiFrame:
     def __init__(self, devices, world, kernel="auto", pipeline="auto"):
         devs = (C.c_int32 * len(devices))(*[int(d) for d in devices])
         self._m = C.c_void_p()
-        st = lib.om_multi_create(devs, len(devices), C.byref(self._m))
+        with _stdout_to_stderr():
+            st = lib.om_multi_create(devs, len(devices), C.byref(self._m))
         if st != L.OM_OK:
             raise L.OmError(f"om_multi_create failed ({st}): {lib.om_multi_last_error(None).decode()}")
         self.n = len(devices)

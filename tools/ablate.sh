@@ -58,6 +58,13 @@ declare -A V=(
   [lpc2k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=2048"
   [lpc8k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=8192"
   [lpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=16384"
+  # r02: Sphere::hit without the divisions when both roots are provably rejected (default on)
+  [nofastrej]="$COMMON $DEV -DOM_SPHERE_FAST_REJECT=0"
+  # r02: async tails (each batch's tail + accumulate on a high-priority tail stream)
+  [async]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1"
+  [aspb4]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_SPB_ASYNC=4"
+  [aspb8]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_SPB_ASYNC=8"
+  [tprio0]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
@@ -71,8 +78,10 @@ fi
 if [ "$1" = build ]; then
   mkdir -p _abl
   for k in ${VARIANTS:-${!V[@]}}; do
-    ( /opt/rocm/bin/hipcc ${V[$k]} -shared -o _abl/lib_$k.so $SRC/om_world.cpp $SRC/om_bvh.cpp $SRC/om_image.cpp $SRC/om_tiles.cpp -x hip $SRC/om_render.hip $SRC/om_wavefront.hip $SRC/om_display.hip \
-      > _abl/$k.log 2>&1 && echo "built $k" ) &
+    ( printf 'extern "C" const char* om_build_id(void) { return "ablate-%s"; }\n' "$k" > _abl/bid_$k.cpp && \
+      /opt/rocm/bin/hipcc ${V[$k]} -shared -o _abl/lib_$k.so $SRC/om_world.cpp $SRC/om_bvh.cpp $SRC/om_image.cpp $SRC/om_tiles.cpp \
+        $SRC/om_shard.cpp _abl/bid_$k.cpp -x hip $SRC/om_render.hip $SRC/om_wavefront.hip $SRC/om_display.hip $SRC/om_multi.hip \
+        -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib > _abl/$k.log 2>&1 && echo "built $k" ) &
   done
   wait
   exit 0
