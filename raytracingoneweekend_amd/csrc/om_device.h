@@ -77,7 +77,7 @@ __device__ __forceinline__ F3 rand_in_unit_sphere(Rng& g) {                     
 
 // ---------------------------------------------------------------- traced.rs
 #ifndef OM_SPHERE_FAST_REJECT
-#define OM_SPHERE_FAST_REJECT 1
+#define OM_SPHERE_FAST_REJECT 0
 #endif
 // Sphere::hit (traced.rs:39-62) up to the accepted root.
 __device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root) {

@@ -58,7 +58,9 @@ declare -A V=(
   [lpc2k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=2048"
   [lpc8k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=8192"
   [lpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=16384"
-  # r02: Sphere::hit without the divisions when both roots are provably rejected (default on)
+  # r02: Sphere::hit without the divisions when both roots are provably rejected (default off:
+  # -0.4% on C1 over two A/B pairs at 32 and 128 spp per call, profiles/r02_v3)
+  [fastrej]="$COMMON $DEV -DOM_SPHERE_FAST_REJECT=1"
   [nofastrej]="$COMMON $DEV -DOM_SPHERE_FAST_REJECT=0"
   # r02: async tails (each batch's tail + accumulate on a high-priority tail stream)
   [async]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1"
