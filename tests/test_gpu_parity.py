@@ -66,6 +66,48 @@ def test_marched_scene_bit_exact(om, oracle, pipeline):
 
 
 @pytest.mark.parametrize("pipeline", PIPELINES)
+def test_marched_scene_many_rays_bit_exact(om, oracle, pipeline):
+    """C2's scene on 0.46 M samples: the lazy march steps (a leading marched sphere alone while
+    every other object's bound stays above it) decide the same winner and the
+    same distance as the full loop of hits.rs:294-332 on every step of every ray."""
+    W, H, SPP = 240, 135, 14
+    got, exp, _ = _render_both(om, oracle, om.marched_scene(), oracle.marched_scene(), om.default_camera(W / H),
+                               oracle.default_camera(W / H), W, H, SPP, "auto", march_steps=256, pipeline=pipeline,
+                               seed=21)
+    nb, msg = compare_stats(got, exp, f"S-marched large/{pipeline}")
+    assert nb == 0, msg
+
+
+def _marched_zoo(om, O):
+    """Marched spheres nested, overlapping and tiny; a box; a NON-uniformly scaled torus (its
+    cull factor bk != 1); the camera inside the big sphere's shell region."""
+    w, ow = om.HittableList.new(), O.World()
+    mats = [(om.Material.new_lambertian((0.6, 0.6, 0.6)), O.material("lambertian", (0.6, 0.6, 0.6))),
+            (om.Material.new_metal_fuzz((0.8, 0.7, 0.5), 0.3), O.material("metal", (0.8, 0.7, 0.5), fuzz=0.3)),
+            (om.Material.new_dielectric(1.5), O.material("dielectric", ior=1.5))]
+    for (c, r, k) in [((0., -100., 0.), 100., 0), ((0., 0.6, 0.), 0.6, 2), ((0., 0.6, 0.), 0.3, 1),
+                      ((0.9, 0.3, 0.2), 0.3, 0), ((-0.7, 0.05, 0.6), 0.05, 1), ((0.35, 0.6, 0.), 0.4, 0)]:
+        w += om.MarchedSphere(c, r, mats[k][0]); ow.add_marched_sphere(c, r, mats[k][1])
+    w += om.MarchedBox((-1.0, 0.4, -0.3), (0.2, 0.4, 0.3), mats[1][0])
+    ow.add_marched_box((-1.0, 0.4, -0.3), (0.2, 0.4, 0.3), mats[1][1])
+    l2w = om.m4x4("TR", 0.2, 1.5, -0.8) ^ om.m4x4("RX", 0.7) ^ om.m4x4("SC", 1.6, 0.6, 1.1)
+    w += om.MarchedTorus.new(l2w, (0.5, 0.12, 0.12), mats[0][0]); ow.add_marched_torus(l2w.to_numpy(), (0.5, 0.12, 0.12), mats[0][1])
+    cam = om.Camera.new((2.2, 1.1, 2.6), (0., 0.5, 0.), (0., 1., 0.), 45., 1.6, 0.05, 3.)
+    ocam = O.camera((2.2, 1.1, 2.6), (0., 0.5, 0.), (0., 1., 0.), 45., 1.6, 0.05, 3.)
+    return w, ow, cam, ocam
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_marched_zoo_bit_exact(om, oracle, pipeline):
+    w, ow, cam, ocam = _marched_zoo(om, oracle)
+    W, H, SPP = 96, 60, 6
+    got, exp, _ = _render_both(om, oracle, w, ow, cam, ocam, W, H, SPP, "auto", march_steps=512, pipeline=pipeline,
+                               seed=5)
+    nb, msg = compare_stats(got, exp, f"marched zoo/{pipeline}")
+    assert nb == 0, msg
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
 def test_adaptive_retirement_bit_exact(om, oracle, pipeline):
     W, H, SPP = 32, 24, 24
     got, exp, _ = _render_both(om, oracle, om.random_scene(0x5EED), oracle.random_scene(0x5EED),
