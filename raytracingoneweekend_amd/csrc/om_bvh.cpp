@@ -207,6 +207,11 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     for (uint32_t gi : always) {
         OmAlwaysRec r;
         r.gi = gi; r.pad = 0;
+        if (gi < fw.offsets[K_SPHERE + 1]) {      // axis-aligned sphere: every off-diagonal entry of W2L is +-0
+            const float* m = fw.sph_test[gi - fw.offsets[K_SPHERE]].w2l;
+            if (m[1] == 0.0f && m[2] == 0.0f && m[4] == 0.0f && m[6] == 0.0f && m[8] == 0.0f && m[9] == 0.0f)
+                r.pad = OM_ALWAYS_DIAG_SPHERE;
+        }
         Box bx;
         bool bounded = true;
         if (gi >= fw.offsets[K_TRI] && gi < fw.offsets[K_TRI + 1]) bx = bary_box(w.triangles[gi - fw.offsets[K_TRI]], false);
@@ -281,7 +286,10 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
                 const OmBvhNode& L = b.nodes[(uint32_t)src.left];
                 const OmBvhNode& R = b.nodes[(uint32_t)src.right];
                 OmBvh2Node o{};
-                for (int i = 0; i < 3; ++i) { o.lo0[i] = L.lo[i]; o.hi0[i] = L.hi[i]; o.lo1[i] = R.lo[i]; o.hi1[i] = R.hi[i]; }
+                for (int i = 0; i < 3; ++i) {
+                    OM_B2_LO(o, 0, i) = L.lo[i]; OM_B2_HI(o, 0, i) = L.hi[i];
+                    OM_B2_LO(o, 1, i) = R.lo[i]; OM_B2_HI(o, 1, i) = R.hi[i];
+                }
                 o.c0 = code((uint32_t)src.left);
                 o.c1 = code((uint32_t)src.right);
                 out[idx] = o;
@@ -293,8 +301,8 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     if (b.nodes[root].left < 0) {            // a single leaf: one node, second child an empty leaf
         OmBvh2Node o{};
         for (int i = 0; i < 3; ++i) {
-            o.lo0[i] = b.nodes[root].lo[i]; o.hi0[i] = b.nodes[root].hi[i];
-            o.lo1[i] = INFINITY; o.hi1[i] = -INFINITY;
+            OM_B2_LO(o, 0, i) = b.nodes[root].lo[i]; OM_B2_HI(o, 0, i) = b.nodes[root].hi[i];
+            OM_B2_LO(o, 1, i) = INFINITY; OM_B2_HI(o, 1, i) = -INFINITY;
         }
         fw.b2leaves.push_back((leaf_first[root] << 8) | (uint32_t)b.nodes[root].right);
         fw.b2leaves.push_back(0u);
@@ -336,7 +344,10 @@ void build_bvh4(FrozenWorld& fw) {
     auto kids = [&](uint32_t n, Ch* out) {
         const OmBvh2Node& N = fw.b2nodes[n];
         out[0].code = N.c0; out[1].code = N.c1;
-        for (int i = 0; i < 3; ++i) { out[0].lo[i] = N.lo0[i]; out[0].hi[i] = N.hi0[i]; out[1].lo[i] = N.lo1[i]; out[1].hi[i] = N.hi1[i]; }
+        for (int i = 0; i < 3; ++i) {
+            out[0].lo[i] = OM_B2_LO(N, 0, i); out[0].hi[i] = OM_B2_HI(N, 0, i);
+            out[1].lo[i] = OM_B2_LO(N, 1, i); out[1].hi[i] = OM_B2_HI(N, 1, i);
+        }
     };
     auto area = [](const Ch& c) {
         const double dx = std::max(0.0, (double)c.hi[0] - c.lo[0]), dy = std::max(0.0, (double)c.hi[1] - c.lo[1]),

@@ -79,10 +79,8 @@ __device__ __forceinline__ F3 rand_in_unit_sphere(Rng& g) {                     
 #ifndef OM_SPHERE_FAST_REJECT
 #define OM_SPHERE_FAST_REJECT 0
 #endif
-// Sphere::hit (traced.rs:39-62) up to the accepted root.
-__device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root) {
-    const F3 lo = xform_p(T.w2l, o);
-    const F3 ld = xform_v(T.w2l, T.dz, d);
+// Sphere::hit (traced.rs:39-62) up to the accepted root, from the ray in local space.
+__device__ __forceinline__ bool sphere_root_local(F3 lo, F3 ld, float tmin, float tmax, float& root) {
     const float a = dot(ld, ld);
     const float half_b = dot(lo, ld);
     const float c = dot(lo, lo) - 1.0f;
@@ -110,6 +108,22 @@ __device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, f
     }
     root = r;
     return true;
+}
+__device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root) {
+    return sphere_root_local(xform_p(T.w2l, o), xform_v(T.w2l, T.dz, d), tmin, tmax, root);
+}
+// The same test for a sphere whose world-to-local block is diagonal (off-diagonal entries
+// exactly +-0: an axis-aligned scaled sphere such as random_scene's ground, main.rs:38-40).
+// Each dropped term of ((m0*x + m1*y) + m2*z) + m3 is a signed zero, and adding a signed zero
+// leaves every nonzero value unchanged, so lo and ld equal the full transform's up to the
+// sign of a zero component.  A zero's sign reaches the roots only as -(+-0) - sqrtd with
+// sqrtd = 0, i.e. a root of +-0, which tmin > 0 rejects either way; everything else
+// (dot products of squares and sums with a nonzero term) is sign-blind.  Callers use it only
+// when tmin > 0; the winner's HitRecord is still built by the full transform.
+__device__ __forceinline__ bool sphere_root_diag(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root) {
+    const F3 lo = f3(T.w2l[0] * o.x + T.w2l[3], T.w2l[5] * o.y + T.w2l[7], T.w2l[10] * o.z + T.w2l[11]);
+    const F3 ld = f3(T.w2l[0] * d.x + T.dz[0], T.w2l[5] * d.y + T.dz[1], T.w2l[10] * d.z + T.dz[2]);
+    return sphere_root_local(lo, ld, tmin, tmax, root);
 }
 // Cube::hit (traced.rs:266-298) up to (smallest_t, idx).
 __device__ __forceinline__ bool cube_root(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root, int& axis) {

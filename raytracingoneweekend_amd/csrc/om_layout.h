@@ -120,14 +120,28 @@ struct OM_ALIGN16 OmAlwaysRec {
     float lo[3];
     uint32_t gi;
     float hi[3];
-    uint32_t pad;
+    uint32_t pad;     // OM_ALWAYS_DIAG_SPHERE: a sphere whose world-to-local block is diagonal
 };
+#define OM_ALWAYS_DIAG_SPHERE 1u
 
 // Compressed binary BVH node (64 B): both child boxes live in the parent, so one
 // node read yields both slab tests.  child = 16-bit code: node index, or
 // OM_LEAF | leaf index; b2leaves[leaf] = (first_record << 8) | count (records =
 // srecs, leaf order).  The traversal stack holds these 16-bit codes.
 #define OM_LEAF 0x8000u
+// OM_PK_SLAB: the box planes interleaved as (lo, hi) pairs per axis, b[6k + 2i] = lo_k[i],
+// b[6k + 2i + 1] = hi_k[i], so one v_pk_fma_f32 gives both slab distances of an axis.
+#ifndef OM_PK_SLAB
+#define OM_PK_SLAB 0
+#endif
+#if OM_PK_SLAB
+struct OM_ALIGN16 OmBvh2Node {
+    float b[12];
+    uint32_t c0, c1, pad0, pad1;
+};
+#define OM_B2_LO(n, k, i) ((n).b[6 * (k) + 2 * (i)])
+#define OM_B2_HI(n, k, i) ((n).b[6 * (k) + 2 * (i) + 1])
+#else
 struct OM_ALIGN16 OmBvh2Node {
     float lo0[3];
     uint32_t c0;
@@ -138,6 +152,9 @@ struct OM_ALIGN16 OmBvh2Node {
     float hi1[3];
     uint32_t pad1;
 };
+#define OM_B2_LO(n, k, i) ((k) == 0 ? (n).lo0[i] : (n).lo1[i])
+#define OM_B2_HI(n, k, i) ((k) == 0 ? (n).hi0[i] : (n).hi1[i])
+#endif
 
 // Device view of a frozen world (passed by value as a kernel argument).
 struct OmSceneDev {

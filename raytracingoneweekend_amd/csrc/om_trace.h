@@ -158,7 +158,11 @@ __device__ __forceinline__ int traced_bvh(const OmSceneDev& S, F3 o, F3 d, float
 }
 
 // The primitives outside the BVH trees (always2): conservative box first, then the
-// exact test with the brute-force tie rule.
+// exact test with the brute-force tie rule.  OM_DIAG_SPHERE: an unbounded record flagged as
+// an axis-aligned sphere takes sphere_root_diag (same accepted root, 24 fewer VALU).
+#ifndef OM_DIAG_SPHERE
+#define OM_DIAG_SPHERE 1
+#endif
 template <class Wk>
 __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, float tmin, float ix, float iy, float iz,
                                               float nox, float noy, float noz, float t_lo, float& closest, int& best, Wk& w) {
@@ -166,7 +170,20 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
         const OmAlwaysRec A = S.always2_rec[k];
 #ifndef OM_ALWAYS2_INF_SLAB
         // an unbounded record (huge primitives, planes: lo = -inf) passes every slab test
-        if (A.lo[0] == -INFINITY) { offer(S, A.gi, o, d, tmin, closest, best, w); continue; }
+        if (A.lo[0] == -INFINITY) {
+#if OM_DIAG_SPHERE
+            if (A.pad == OM_ALWAYS_DIAG_SPHERE && tmin > 0.0f) {                // axis-aligned sphere (the ground)
+                float t;
+                w.add_prim();
+                if (sphere_root_diag(S.sph_test[A.gi], o, d, tmin, closest, t) && (t < closest || (int)A.gi > best)) {
+                    closest = t; best = (int)A.gi;
+                }
+                continue;
+            }
+#endif
+            offer(S, A.gi, o, d, tmin, closest, best, w);
+            continue;
+        }
 #endif
         w.add_pre();
         const float t_hi = closest * 1.0001f + 1e-3f;
@@ -546,6 +563,20 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
         const OmBvh2Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
         w.add_pre(2);
         const float t_hi = closest * 1.0001f + 1e-3f;
+#if OM_PK_SLAB
+        // (lo, hi) plane pairs: one v_pk_fma_f32 per axis and box (same fma per lane)
+        typedef float pkf2 __attribute__((ext_vector_type(2)));
+        const pkf2* B = (const pkf2*)N.b;
+        const pkf2 IX = {ix, ix}, IY = {iy, iy}, IZ = {iz, iz}, OX = {nox, nox}, OY = {noy, noy}, OZ = {noz, noz};
+        pkf2 X = __builtin_elementwise_fma(B[0], IX, OX), Y = __builtin_elementwise_fma(B[1], IY, OY),
+             Z = __builtin_elementwise_fma(B[2], IZ, OZ);
+        const float n0 = slab_near(X.x, X.y, Y.x, Y.y, Z.x, Z.y, t_lo);
+        const float f0 = slab_far(X.x, X.y, Y.x, Y.y, Z.x, Z.y, t_hi);
+        X = __builtin_elementwise_fma(B[3], IX, OX); Y = __builtin_elementwise_fma(B[4], IY, OY);
+        Z = __builtin_elementwise_fma(B[5], IZ, OZ);
+        const float n1 = slab_near(X.x, X.y, Y.x, Y.y, Z.x, Z.y, t_lo);
+        const float f1 = slab_far(X.x, X.y, Y.x, Y.y, Z.x, Z.y, t_hi);
+#else
         float x0 = __builtin_fmaf(N.lo0[0], ix, nox), x1 = __builtin_fmaf(N.hi0[0], ix, nox);
         float y0 = __builtin_fmaf(N.lo0[1], iy, noy), y1 = __builtin_fmaf(N.hi0[1], iy, noy);
         float z0 = __builtin_fmaf(N.lo0[2], iz, noz), z1 = __builtin_fmaf(N.hi0[2], iz, noz);
@@ -556,6 +587,7 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
         z0 = __builtin_fmaf(N.lo1[2], iz, noz); z1 = __builtin_fmaf(N.hi1[2], iz, noz);
         const float n1 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
         const float f1 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
+#endif
         const bool h0 = !(n0 > f0), h1 = !(n1 > f1);
         if (h0 && h1) {                                 // near child next, far child pushed
             const bool swap = n1 < n0;

@@ -66,6 +66,11 @@ declare -A V=(
   [async]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1"
   [aspb4]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_SPB_ASYNC=4"
   [aspb8]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_SPB_ASYNC=8"
+  # r02: the axis-aligned ground sphere's diagonal test (default on); packed slab FMAs on the
+  # interleaved BVH2 node layout
+  [nodiag]="$COMMON $DEV -DOM_DIAG_SPHERE=0"
+  [pkslab]="$COMMON $DEV -DOM_PK_SLAB=1"
+  [pkslabl]="$COMMON $DEV -DOM_PK_SLAB=1 -DOM_WF_EARLY_REST=0"
   [tprio0]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
