@@ -12,10 +12,10 @@ timeout -k 10 400 python -m pytest tests -m gpu -x -q -p no:cacheprovider > "$OU
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 || { echo "smoke failed"; exit 1; }
 timeout -k 10 300 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" || { echo "bench failed"; exit 1; }
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python bench.py --no-cpu-baseline > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { echo "rocprof failed"; exit 1; }
-timeout -k 10 300 python bench.py --no-cpu-baseline --kernel-timing launch > "$OUT/bench_launch_timing.json" 2>> "$OUT/bench.err" || { echo "bench (launch timing) failed"; exit 1; }
-timeout -k 10 300 python bench.py --no-cpu-baseline --kernel-timing off > "$OUT/bench_notiming.json" 2>> "$OUT/bench.err" || { echo "bench (no timing) failed"; exit 1; }
+    python bench.py --no-cpu-baseline --no-extras > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" || { echo "rocprof failed"; exit 1; }
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --kernel-timing launch > "$OUT/bench_launch_timing.json" 2>> "$OUT/bench.err" || { echo "bench (launch timing) failed"; exit 1; }
+timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --kernel-timing off > "$OUT/bench_notiming.json" 2>> "$OUT/bench.err" || { echo "bench (no timing) failed"; exit 1; }
 if [ -z "$NO_PMC" ]; then
-  bash tools/pmc.sh "$TAG/pmc" > "$OUT/pmc.log" 2>&1 || { echo "pmc failed"; exit 1; }
+  bash tools/pmc.sh "$TAG/pmc" --no-extras > "$OUT/pmc.log" 2>&1 || { echo "pmc failed"; exit 1; }
 fi
 echo ok
