@@ -18,8 +18,9 @@ torch.distributed (gloo, host memory) is the harness's control plane only: it ha
 unique id from rank 0 to the others, and carries the barriers and the max-over-ranks time.
 
 At N=1 the line also carries `configs`: C2 (marched SDF scene, 256 march steps) and C3 (10k
-spheres, BVH) at full spp with their own roofline and CPU baseline, and C0 (the reference's
-CPU case, 400x225x64 at depth 8) timed on the GPU and on the host cores.
+spheres, BVH) at full spp with their own roofline and CPU baseline, C4's 3840x2160 frame at
+256 spp (the N=1 leg of the 8-GPU config), and C0 (the reference's CPU case, 400x225x64 at
+depth 8) timed on the GPU and on the host cores.
 
 Output: ONE JSON line on rank 0 (see DESIGN.md §7 for every field).
 """
@@ -337,6 +338,14 @@ def main():
                             "workload": workload(name, e), "pipeline": "megakernel" if e["mega"] else "wavefront",
                             "roofline": e["roofline"], "work": e["work"],
                             "cpu_baseline": cpu_baseline(name, min(8.0, args.cpu_budget))}
+        # C4's 4K frame at N=1: 8 steps of 32 spp (256 of the config's 4096 spp; the full frame is
+        # the multi-GPU run, --config C4), so the driver's line exercises the 3840x2160 frame too
+        e = run_config("C4", args, ctl, local_rank, 8, 1, args.spp_per_step, "span")
+        extras["C4"] = {"metric": "Msamples/s", "value": e["value"], "ms_per_step": round(e["elapsed_s"] / e["steps"] * 1e3, 4),
+                        "workload": workload("C4", e) + " (N=1 leg of the 8-GPU config: 256 of its 4096 spp)",
+                        "pipeline": "megakernel" if e["mega"] else "wavefront",
+                        "roofline": e["roofline"], "work": e["work"],
+                        "cpu_baseline": cpu_baseline("C4", min(6.0, args.cpu_budget))}
         extras["C0"] = run_c0(args)
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
