@@ -547,6 +547,10 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     } else if ((mode == OM_KERNEL_BVH2 || mode == OM_KERNEL_BVH4) && c->scene.n_b2nodes) {
         const uint32_t lds = kBlock * c->scene.b2_stack * 2u + c->scene.b2_lds_bytes;
         go<MODE_BVH2, kBlock>(count, threads, lds, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
+    } else if ((mode == OM_KERNEL_BVH2 || mode == OM_KERNEL_BVH4) && c->scene.n_bvh_nodes <= 1u) {
+        // empty BVH2 and at most one leaf in the old BVH (marched-only worlds): the reference
+        // loop, without MODE_BVH's scratch-memory stack
+        go<MODE_BRUTE, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
     } else {
         go<MODE_BVH, kBlock>(count, threads, 0, stream, c->scene, C, P, jt, dev_stats, dev_pixels, ctr);
     }

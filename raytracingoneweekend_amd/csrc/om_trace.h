@@ -374,19 +374,65 @@ __device__ __forceinline__ bool march_begin(const M& m, F3 o, F3 d, float tmin, 
     return true;
 }
 
+// Escape test: true when no point the march can still visit lies within HIT
+// of a marched object, so the march ends without a hit whatever its remaining steps do —
+// and a miss's result does not depend on t or on how many steps ran (hits.rs:294-332: the
+// traced `closest`/winner stand).  Per object: a centre c and a radius rho such that every
+// computed point with |p - c| > rho has computed |sdf| > HIT (sphere: (r + HIT)(1 + 1e-5) +
+// 1e-5 covers the <= 4u error of |p - c| - r; box and torus: their march-cull bounds with
+// best = HIT).  The march's future points lie within e_p <= 4u(|o|_1 + T) of the half-line
+// {p + d s, s >= 0}, T = min(tmax, closest) > t (hits.rs:294), so it suffices that the
+// half-line's closest approach to c, sqrt(|w|^2 - min(d.w, 0)^2) with w = p - c, exceeds
+// rho + 2e-6(|o|_1 + T) (2.5x the two e_p), after a 1e-5 |w|^2 allowance for the f32
+// evaluation of the squared approach (<= 12u |w|^2).  Infinite T, NaN or inf anywhere:
+// false.  The test never touches output bits, so it may round freely within those margins.
+#ifndef OM_MARCH_ESCAPE
+#define OM_MARCH_ESCAPE 0
+#endif
+template <class M>
+__device__ __forceinline__ bool march_escapes(const M& m, F3 o, F3 d, F3 p, float T) {
+    const float HIT = 0.001f;
+    const float E = 2e-6f * (((fabsf(o.x) + fabsf(o.y)) + fabsf(o.z)) + T);
+    bool esc = true;
+    auto clear = [&](float cx, float cy, float cz, float rho) {
+        const float wx = p.x - cx, wy = p.y - cy, wz = p.z - cz;
+        const float ww = wx * wx + wy * wy + wz * wz;
+        const float pm = fminf(d.x * wx + d.y * wy + d.z * wz, 0.0f);
+        const float a = rho + E;
+        esc = esc && (ww - pm * pm) - 1e-5f * ww > a * a;
+    };
+    for_objects<M::KS>(m.ns, [&](uint32_t i) {
+        const OmMSphere& Q = m.s[i];
+        clear(Q.center[0], Q.center[1], Q.center[2], (Q.radius + HIT) * 1.00001f + 1e-5f);
+    });
+    for_objects<M::KB>(m.nb, [&](uint32_t i) {
+        const OmMBox& B = m.b[i];
+        clear(B.center[0], B.center[1], B.center[2], (HIT + B.br) * 1.0001f);
+    });
+    for_objects<M::KT>(m.nt, [&](uint32_t i) {
+        const OmMTorus& Q = m.t[i];
+        clear(Q.bc[0], Q.bc[1], Q.bc[2], HIT * Q.bk + Q.br);
+    });
+    return esc;
+}
+
 // One iteration of the sphere-tracing loop (hits.rs:294-332).  Returns 0 to continue, 1 on
 // a hit (gi = the marched winner's global index, the hit is at t), 2 when the march ends
-// without one.
+// without one.  Every 4th step first runs the escape test above (2: the same miss, sooner).
 template <class M, class Wk>
 __device__ __forceinline__ int march_step(const OmSceneDev& S, const M& m, F3 o, F3 d, float tmax, float closest, float& t,
                                           uint32_t& iters, int& gi, Wk& w) {
     const float HIT = 0.001f;
     if (!(t < tmax && t < closest && iters > 0)) return 2;                    // hits.rs:294
+    const F3 p = at(o, d, t);
+#if OM_MARCH_ESCAPE
+    if ((iters & 3u) == 0u && march_escapes(m, o, d, p, fminf(tmax, closest))) return 2;
+#endif
     iters -= 1;
     w.add_march();
     int bk;
     uint32_t bi;
-    const float best = nearest_marched(m, at(o, d, t), bk, bi);
+    const float best = nearest_marched(m, p, bk, bi);
     if (bk < 0) return 2;                                                      // hits.rs:323
     if (best < HIT) {                                                          // hits.rs:325-327
         gi = (int)(bk == 0 ? S.off_msph + bi : bk == 1 ? S.off_mbox + bi : S.off_mtor + bi);

@@ -58,6 +58,9 @@ void Buffers::release() {
 namespace {
 
 constexpr uint32_t kNoSample = 0xFFFFFFFFu;
+#ifndef OM_EMPTY_B2_BRUTE
+#define OM_EMPTY_B2_BRUTE 1
+#endif
 enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL = 5, TR_BVH2_LDS = 6, TR_BVH2_GLOBAL = 7,
        TR_BVH4_LDS = 8, TR_BVH4_GLOBAL = 9 };
 // Workgroup = one queue segment.  512 lanes share one LDS copy of the BVH2 nodes between 8
@@ -894,7 +897,11 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
     int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
     if (tr == TR_BVH4_LDS) tr = L.S.n_b4nodes == 0 ? TR_BVH2_LDS : (L.S.b4_lds_bytes ? TR_BVH4_LDS : TR_BVH4_GLOBAL);
-    if (tr == TR_BVH2_LDS) tr = L.S.n_b2nodes == 0 ? TR_BVH : (L.S.b2_lds_bytes ? TR_BVH2_LDS : TR_BVH2_GLOBAL);
+    // an empty BVH2 (no bounded sphere/cube: marched-only worlds, C2) takes the reference loop
+    // when the old BVH holds at most one leaf: TR_BVH's 64-entry stack lives in scratch memory,
+    // which every k_march / k_tail wave would then carry for nothing
+    if (tr == TR_BVH2_LDS)
+        tr = L.S.n_b2nodes == 0 ? (OM_EMPTY_B2_BRUTE && L.S.n_bvh_nodes <= 1u ? TR_BRUTE : TR_BVH) : (L.S.b2_lds_bytes ? TR_BVH2_LDS : TR_BVH2_GLOBAL);
     const uint32_t lds = tr == TR_BVH2_LDS ? stack_bytes<TR_BVH2_LDS>(L.S) + L.S.b2_lds_bytes
                        : tr == TR_BVH2_GLOBAL ? stack_bytes<TR_BVH2_GLOBAL>(L.S) + hyb_nodes(L.S) * 64u
                        : tr == TR_BVH4_LDS ? stack_bytes<TR_BVH4_LDS>(L.S) + L.S.b4_lds_bytes

@@ -71,6 +71,12 @@ declare -A V=(
   [nodiag]="$COMMON $DEV -DOM_DIAG_SPHERE=0"
   [pkslab]="$COMMON $DEV -DOM_PK_SLAB=1"
   [pkslabl]="$COMMON $DEV -DOM_PK_SLAB=1 -DOM_WF_EARLY_REST=0"
+  # r03: march escape test (default off: C2 -35% march steps, time neutral, profiles/r03_v1)
+  [noesc]="$COMMON $DEV -DOM_MARCH_ESCAPE=0"
+  [esc]="$COMMON $DEV -DOM_MARCH_ESCAPE=1"
+  [escregs]="$COMMON $DEV -DOM_MARCH_ESCAPE=1 -DOM_WF_MARCH_REGS=1"
+  # r03: marched-only worlds trace with the scratch-stack BVH instead of the reference loop
+  [bvhfb]="$COMMON $DEV -DOM_EMPTY_B2_BRUTE=0"
   [tprio0]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
