@@ -71,7 +71,7 @@ declare -A V=(
   [nodiag]="$COMMON $DEV -DOM_DIAG_SPHERE=0"
   [pkslab]="$COMMON $DEV -DOM_PK_SLAB=1"
   [pkslabl]="$COMMON $DEV -DOM_PK_SLAB=1 -DOM_WF_EARLY_REST=0"
-  # r03: march escape test (default off: C2 -35% march steps, time neutral, profiles/r03_v1)
+  # r03: march escape test (default off: C2 -35% march steps, time neutral, profiles/r02_v8)
   [noesc]="$COMMON $DEV -DOM_MARCH_ESCAPE=0"
   [esc]="$COMMON $DEV -DOM_MARCH_ESCAPE=1"
   [escregs]="$COMMON $DEV -DOM_MARCH_ESCAPE=1 -DOM_WF_MARCH_REGS=1"
