@@ -312,8 +312,64 @@ __device__ __forceinline__ void for_objects(uint32_t n, F body) {
 // (the first minimum wins; hits.rs:296-322, 341-358).  An object whose conservative lower
 // bound (om_world.cpp) proves |sdf| > best cannot be the new minimum and is skipped: the
 // result is bit-identical to evaluating every SDF.  -> best (INFINITY if none), kind, index.
+//
+// OM_MARCH_PREFETCH (arrays view, measured and off: C2 -17%): every object's
+// parameters are scalar loads that the loop's hit-buffer stores keep the compiler from
+// hoisting, so each object costs a load round trip (s_load + s_waitcnt) before its SDF.  The
+// pipelined form issues the first sphere, box and torus-cull loads together at the top of the
+// step and each type's next object before the current one's SDF (clamped index: always in
+// range, no branch); same objects, same order, same arithmetic.  Empty types read a zero
+// dummy object that no loop iteration uses.
+#ifndef OM_MARCH_PREFETCH
+#define OM_MARCH_PREFETCH 0
+#endif
+static __device__ const OmMSphere kNoMSphere = {};
+static __device__ const OmMBox kNoMBox = {};
+static __device__ const OmMTorus kNoMTorus = {};
+struct TorusCull { float x, y, z, bk, br; };
+__device__ __forceinline__ TorusCull torus_cull(const OmMTorus& T) { return TorusCull{T.bc[0], T.bc[1], T.bc[2], T.bk, T.br}; }
+
+__device__ __forceinline__ float nearest_marched_pf(const MarchedArrays& m, F3 p, int& bk, uint32_t& bi) {
+    float best = INFINITY;
+    bk = -1; bi = 0;
+    const OmMSphere* S = m.ns ? m.s : &kNoMSphere;
+    const OmMBox* B = m.nb ? m.b : &kNoMBox;
+    const OmMTorus* T = m.nt ? m.t : &kNoMTorus;
+    OmMSphere sc = S[0];
+    OmMBox bc = B[0];
+    TorusCull tc = torus_cull(T[0]);
+    for (uint32_t i = 0; i < m.ns; ++i) {
+        const OmMSphere sn = S[i + 1u < m.ns ? i + 1u : i];
+        const float v = fabsf(msphere_sdf(sc, p));
+        if (v < best) { best = v; bk = 0; bi = i; }
+        sc = sn;
+    }
+    for (uint32_t i = 0; i < m.nb; ++i) {
+        const OmMBox bn = B[i + 1u < m.nb ? i + 1u : i];
+        const float dx = p.x - bc.center[0], dy = p.y - bc.center[1], dz = p.z - bc.center[2];
+        const float thr = (best + bc.br) * 1.0001f;                            // inf/NaN -> evaluate
+        if (!(dx * dx + dy * dy + dz * dz > thr * thr)) {
+            const float v = fabsf(mbox_sdf(bc, p));
+            if (v < best) { best = v; bk = 1; bi = i; }
+        }
+        bc = bn;
+    }
+    for (uint32_t i = 0; i < m.nt; ++i) {
+        const TorusCull tn = torus_cull(T[i + 1u < m.nt ? i + 1u : i]);
+        const float dx = p.x - tc.x, dy = p.y - tc.y, dz = p.z - tc.z;
+        const float thr = best * tc.bk + tc.br;                                // inf/NaN -> evaluate
+        if (!(dx * dx + dy * dy + dz * dz > thr * thr)) {
+            const float v = fabsf(mtorus_sdf(T[i], p));
+            if (v < best) { best = v; bk = 2; bi = i; }
+        }
+        tc = tn;
+    }
+    return best;
+}
+
 template <class M>
 __device__ __forceinline__ float nearest_marched(const M& m, F3 p, int& bk, uint32_t& bi) {
+    if constexpr (OM_MARCH_PREFETCH && M::KS == 0u) return nearest_marched_pf(m, p, bk, bi);
     float best = INFINITY;
     bk = -1; bi = 0;
     for_objects<M::KS>(m.ns, [&](uint32_t i) {

@@ -74,6 +74,8 @@ declare -A V=(
   # r03: march escape test (default off: C2 -35% march steps, time neutral, profiles/r02_v8)
   [noesc]="$COMMON $DEV -DOM_MARCH_ESCAPE=0"
   [esc]="$COMMON $DEV -DOM_MARCH_ESCAPE=1"
+  # r02: software-pipelined marched-object loads in the march step (default off: C2 -17%)
+  [pf]="$COMMON $DEV -DOM_MARCH_PREFETCH=1"
   [escregs]="$COMMON $DEV -DOM_MARCH_ESCAPE=1 -DOM_WF_MARCH_REGS=1"
   # r03: marched-only worlds trace with the scratch-stack BVH instead of the reference loop
   [bvhfb]="$COMMON $DEV -DOM_EMPTY_B2_BRUTE=0"
