@@ -313,7 +313,7 @@ __device__ __forceinline__ void for_objects(uint32_t n, F body) {
 // bound (om_world.cpp) proves |sdf| > best cannot be the new minimum and is skipped: the
 // result is bit-identical to evaluating every SDF.  -> best (INFINITY if none), kind, index.
 //
-// OM_MARCH_PREFETCH (arrays view, measured and off: C2 -17%): every object's
+// OM_MARCH_PREFETCH (arrays view, measured and off: C2 -7%): every object's
 // parameters are scalar loads that the loop's hit-buffer stores keep the compiler from
 // hoisting, so each object costs a load round trip (s_load + s_waitcnt) before its SDF.  The
 // pipelined form issues the first sphere, box and torus-cull loads together at the top of the
@@ -326,8 +326,26 @@ __device__ __forceinline__ void for_objects(uint32_t n, F body) {
 static __device__ const OmMSphere kNoMSphere = {};
 static __device__ const OmMBox kNoMBox = {};
 static __device__ const OmMTorus kNoMTorus = {};
+// Loads through the constant address space: always scalar (s_load), whatever the loop stores,
+// so the next object's parameters can be in flight while the current SDF runs.  The scene
+// arrays are immutable while a kernel runs (om_upload_world between calls only).
+typedef const __attribute__((address_space(4))) float om_cfloat;
+__device__ __forceinline__ om_cfloat* cptr(const void* q) { return (om_cfloat*)q; }
+struct SphereP { float x, y, z, r; };
+struct BoxP { float cx, cy, cz, sx, sy, sz, br; };
 struct TorusCull { float x, y, z, bk, br; };
-__device__ __forceinline__ TorusCull torus_cull(const OmMTorus& T) { return TorusCull{T.bc[0], T.bc[1], T.bc[2], T.bk, T.br}; }
+__device__ __forceinline__ SphereP load_sphere(const OmMSphere* q) {
+    om_cfloat* f = cptr(q);
+    return SphereP{f[0], f[1], f[2], f[3]};
+}
+__device__ __forceinline__ BoxP load_box(const OmMBox* q) {
+    om_cfloat* f = cptr(q);
+    return BoxP{f[0], f[1], f[2], f[4], f[5], f[6], f[7]};
+}
+__device__ __forceinline__ TorusCull load_torus_cull(const OmMTorus* q) {
+    om_cfloat* f = cptr(q->bc);
+    return TorusCull{f[0], f[1], f[2], f[3], f[4]};
+}
 
 __device__ __forceinline__ float nearest_marched_pf(const MarchedArrays& m, F3 p, int& bk, uint32_t& bi) {
     float best = INFINITY;
@@ -335,27 +353,32 @@ __device__ __forceinline__ float nearest_marched_pf(const MarchedArrays& m, F3 p
     const OmMSphere* S = m.ns ? m.s : &kNoMSphere;
     const OmMBox* B = m.nb ? m.b : &kNoMBox;
     const OmMTorus* T = m.nt ? m.t : &kNoMTorus;
-    OmMSphere sc = S[0];
-    OmMBox bc = B[0];
-    TorusCull tc = torus_cull(T[0]);
+    SphereP sc = load_sphere(S);
+    BoxP bc = load_box(B);
+    TorusCull tc = load_torus_cull(T);
     for (uint32_t i = 0; i < m.ns; ++i) {
-        const OmMSphere sn = S[i + 1u < m.ns ? i + 1u : i];
-        const float v = fabsf(msphere_sdf(sc, p));
+        const SphereP sn = load_sphere(S + (i + 1u < m.ns ? i + 1u : i));
+        OmMSphere Q;
+        Q.center[0] = sc.x; Q.center[1] = sc.y; Q.center[2] = sc.z; Q.radius = sc.r;
+        const float v = fabsf(msphere_sdf(Q, p));
         if (v < best) { best = v; bk = 0; bi = i; }
         sc = sn;
     }
     for (uint32_t i = 0; i < m.nb; ++i) {
-        const OmMBox bn = B[i + 1u < m.nb ? i + 1u : i];
-        const float dx = p.x - bc.center[0], dy = p.y - bc.center[1], dz = p.z - bc.center[2];
+        const BoxP bn = load_box(B + (i + 1u < m.nb ? i + 1u : i));
+        const float dx = p.x - bc.cx, dy = p.y - bc.cy, dz = p.z - bc.cz;
         const float thr = (best + bc.br) * 1.0001f;                            // inf/NaN -> evaluate
         if (!(dx * dx + dy * dy + dz * dz > thr * thr)) {
-            const float v = fabsf(mbox_sdf(bc, p));
+            OmMBox Q;
+            Q.center[0] = bc.cx; Q.center[1] = bc.cy; Q.center[2] = bc.cz; Q.pad0 = 0.0f;
+            Q.sizes[0] = bc.sx; Q.sizes[1] = bc.sy; Q.sizes[2] = bc.sz; Q.br = bc.br;
+            const float v = fabsf(mbox_sdf(Q, p));
             if (v < best) { best = v; bk = 1; bi = i; }
         }
         bc = bn;
     }
     for (uint32_t i = 0; i < m.nt; ++i) {
-        const TorusCull tn = torus_cull(T[i + 1u < m.nt ? i + 1u : i]);
+        const TorusCull tn = load_torus_cull(T + (i + 1u < m.nt ? i + 1u : i));
         const float dx = p.x - tc.x, dy = p.y - tc.y, dz = p.z - tc.z;
         const float thr = best * tc.bk + tc.br;                                // inf/NaN -> evaluate
         if (!(dx * dx + dy * dy + dz * dz > thr * thr)) {

@@ -74,11 +74,15 @@ declare -A V=(
   # r03: march escape test (default off: C2 -35% march steps, time neutral, profiles/r02_v8)
   [noesc]="$COMMON $DEV -DOM_MARCH_ESCAPE=0"
   [esc]="$COMMON $DEV -DOM_MARCH_ESCAPE=1"
-  # r02: software-pipelined marched-object loads in the march step (default off: C2 -17%)
+  # r02: software-pipelined marched-object loads in the march step (default off: C2 -7%)
   [pf]="$COMMON $DEV -DOM_MARCH_PREFETCH=1"
   [escregs]="$COMMON $DEV -DOM_MARCH_ESCAPE=1 -DOM_WF_MARCH_REGS=1"
   # r03: marched-only worlds trace with the scratch-stack BVH instead of the reference loop
   [bvhfb]="$COMMON $DEV -DOM_EMPTY_B2_BRUTE=0"
+  # r02: LLVM AMDGPU scheduler strategies (same code, different instruction order)
+  [ilp]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-ilp"
+  [memclause]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-memory-clause"
+  [bias0]="$COMMON $DEV -mllvm -amdgpu-schedule-metric-bias=0"
   [tprio0]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
