@@ -163,6 +163,12 @@ __host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
 #ifndef OM_WF_LANES_PER_CU
 #define OM_WF_LANES_PER_CU 4096
 #endif
+// Marched worlds (split march pipeline) use more, smaller-share segments:
+// k_march's lane refill drains a segment at its own pace, and more segments per CU keep the
+// workgroup rounds short.  C2: 2048 / 4096 / 8192 / 16384 lanes per CU.
+#ifndef OM_WF_LANES_PER_CU_MARCH
+#define OM_WF_LANES_PER_CU_MARCH 8192
+#endif
 #ifndef OM_WF_ALIGN
 #define OM_WF_ALIGN 64
 #endif
@@ -890,7 +896,9 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint64_t max_paths = (uint64_t)n_px * batch;
     // segments: ~4096 lanes per CU (16 workgroups of 256), a multiple of the tail grouping
-    uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (OM_WF_LANES_PER_CU / kBlk));
+    const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
+    const uint32_t lanes_per_cu = march ? OM_WF_LANES_PER_CU_MARCH : OM_WF_LANES_PER_CU;
+    uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (lanes_per_cu / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
     const uint32_t segcap = seg_capacity(max_paths, nseg);
     hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg, (int)nsets);
@@ -906,7 +914,6 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
                        : tr == TR_BVH2_GLOBAL ? stack_bytes<TR_BVH2_GLOBAL>(L.S) + hyb_nodes(L.S) * 64u
                        : tr == TR_BVH4_LDS ? stack_bytes<TR_BVH4_LDS>(L.S) + L.S.b4_lds_bytes
                        : tr == TR_BVH4_GLOBAL ? stack_bytes<TR_BVH4_GLOBAL>(L.S) : 0u;
-    const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
     Gen R;
     R.C = L.C; R.jitter = L.jitter; R.stats = L.stats; R.pixels = L.pixels; R.n_pixels = n_px;
     R.by_pixel = L.stats_by_pixel ? 1u : 0u;
