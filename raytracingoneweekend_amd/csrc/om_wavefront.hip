@@ -163,11 +163,12 @@ __host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
 #ifndef OM_WF_LANES_PER_CU
 #define OM_WF_LANES_PER_CU 4096
 #endif
-// Marched worlds (split march pipeline) use more, smaller-share segments:
-// k_march's lane refill drains a segment at its own pace, and more segments per CU keep the
-// workgroup rounds short.  C2: 2048 / 4096 / 8192 / 16384 lanes per CU.
-#ifndef OM_WF_LANES_PER_CU_MARCH
-#define OM_WF_LANES_PER_CU_MARCH 8192
+// Marched worlds (split march pipeline) and BVH2s read through L2 (S-10k)
+// use twice the segments: k_march's lane refill and the L2-bound traversal both drain a
+// segment at their own pace, and halving each workgroup's share shortens the last round of
+// workgroups in every launch.  C2 / C3 / C1 measurements in DESIGN.md §5.8.
+#ifndef OM_WF_LANES_PER_CU_WIDE
+#define OM_WF_LANES_PER_CU_WIDE 8192
 #endif
 #ifndef OM_WF_ALIGN
 #define OM_WF_ALIGN 64
@@ -895,14 +896,6 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const uint64_t max_paths = (uint64_t)n_px * batch;
-    // segments: ~4096 lanes per CU (16 workgroups of 256), a multiple of the tail grouping
-    const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
-    const uint32_t lanes_per_cu = march ? OM_WF_LANES_PER_CU_MARCH : OM_WF_LANES_PER_CU;
-    uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (lanes_per_cu / kBlk));
-    nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
-    const uint32_t segcap = seg_capacity(max_paths, nseg);
-    hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg, (int)nsets);
-    if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
     int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
     if (tr == TR_BVH4_LDS) tr = L.S.n_b4nodes == 0 ? TR_BVH2_LDS : (L.S.b4_lds_bytes ? TR_BVH4_LDS : TR_BVH4_GLOBAL);
     // an empty BVH2 (no bounded sphere/cube: marched-only worlds, C2) takes the reference loop
@@ -910,6 +903,15 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     // which every k_march / k_tail wave would then carry for nothing
     if (tr == TR_BVH2_LDS)
         tr = L.S.n_b2nodes == 0 ? (OM_EMPTY_B2_BRUTE && L.S.n_bvh_nodes <= 1u ? TR_BRUTE : TR_BVH) : (L.S.b2_lds_bytes ? TR_BVH2_LDS : TR_BVH2_GLOBAL);
+    // segments, a multiple of the tail grouping: 4096 lanes per CU (8 workgroups of 512) for
+    // traced worlds whose BVH2 sits in LDS, 8192 for marched worlds and L2-resident trees
+    const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
+    const uint32_t lanes_per_cu = (march || tr == TR_BVH2_GLOBAL) ? OM_WF_LANES_PER_CU_WIDE : OM_WF_LANES_PER_CU;
+    uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (lanes_per_cu / kBlk));
+    nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
+    const uint32_t segcap = seg_capacity(max_paths, nseg);
+    hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg, (int)nsets);
+    if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
     const uint32_t lds = tr == TR_BVH2_LDS ? stack_bytes<TR_BVH2_LDS>(L.S) + L.S.b2_lds_bytes
                        : tr == TR_BVH2_GLOBAL ? stack_bytes<TR_BVH2_GLOBAL>(L.S) + hyb_nodes(L.S) * 64u
                        : tr == TR_BVH4_LDS ? stack_bytes<TR_BVH4_LDS>(L.S) + L.S.b4_lds_bytes

@@ -58,10 +58,9 @@ declare -A V=(
   [lpc2k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=2048"
   [lpc8k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=8192"
   [lpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=16384"
-  # r02: lanes per CU for marched worlds only (default 8192)
-  [mlpc4k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_MARCH=4096"
-  [mlpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_MARCH=16384"
-  [mlpc32k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_MARCH=32768"
+  # r02: lanes per CU for marched worlds and L2-resident BVH2s (default 8192)
+  [mlpc4k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_WIDE=4096"
+  [mlpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_WIDE=16384"
   # r02: Sphere::hit without the divisions when both roots are provably rejected (default off:
   # -0.4% on C1 over two A/B pairs at 32 and 128 spp per call, profiles/r02_v3)
   [fastrej]="$COMMON $DEV -DOM_SPHERE_FAST_REJECT=1"
