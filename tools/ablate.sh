@@ -61,6 +61,10 @@ declare -A V=(
   # r02: lanes per CU for marched worlds and L2-resident BVH2s (default 8192)
   [mlpc4k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_WIDE=4096"
   [mlpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_WIDE=16384"
+  [w6k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_WIDE=6144"
+  [w12k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_WIDE=12288"
+  [lpc6k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=6144"
+  [lpc3k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=3072"
   # r02: Sphere::hit without the divisions when both roots are provably rejected (default off:
   # -0.4% on C1 over two A/B pairs at 32 and 128 spp per call, profiles/r02_v3)
   [fastrej]="$COMMON $DEV -DOM_SPHERE_FAST_REJECT=1"
