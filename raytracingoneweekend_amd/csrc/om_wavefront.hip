@@ -73,6 +73,16 @@ enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL 
 #ifndef OM_WF_WAVES
 #define OM_WF_WAVES 8
 #endif
+// bounce 0 (coherent camera rays, VALU-issue-bound) may ask for fewer waves, and so more
+// registers, than the latency-bound later bounces
+#ifndef OM_WF_WAVES_FIRST
+#define OM_WF_WAVES_FIRST OM_WF_WAVES
+#endif
+#if OM_WF_WAVES > 0 && OM_WF_WAVES_FIRST > 0
+#define OM_WAVES_ATTR_B(FIRST) __attribute__((amdgpu_waves_per_eu((FIRST) ? OM_WF_WAVES_FIRST : OM_WF_WAVES, (FIRST) ? OM_WF_WAVES_FIRST : OM_WF_WAVES)))
+#else
+#define OM_WAVES_ATTR_B(FIRST)
+#endif
 #if OM_WF_WAVES > 0                                               // occupancy request (waves per SIMD)
 #define OM_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(OM_WF_WAVES, OM_WF_WAVES)))
 #else
@@ -401,7 +411,7 @@ __device__ __forceinline__ bool gen_path(const OmParamsDev& P, const Gen& R, uin
 // HIT (split march pipeline): no trace here; the (closest, winner) of every path of the
 // segment was written to `hitbuf` (queue-slot order) by k_march.
 template <int TR, bool COUNT, bool MARCH, bool FIRST, bool HIT = false>
-__global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmParamsDev P, Seg G, Gen R, Queue in,
+__global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneDev S, OmParamsDev P, Seg G, Gen R, Queue in,
                                                  const uint32_t* __restrict__ count_in, Queue out,
                                                  uint32_t* __restrict__ count_out, float4* __restrict__ res,
                                                  uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters,

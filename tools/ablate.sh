@@ -63,6 +63,9 @@ declare -A V=(
   [mlpc16k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_WIDE=16384"
   [w6k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_WIDE=6144"
   [w12k]="$COMMON $DEV -DOM_WF_LANES_PER_CU_WIDE=12288"
+  # r02: bounce 0's occupancy request (waves per SIMD; default = OM_WF_WAVES)
+  [first7]="$COMMON $DEV -DOM_WF_WAVES_FIRST=7"
+  [first6]="$COMMON $DEV -DOM_WF_WAVES_FIRST=6"
   [lpc6k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=6144"
   [lpc3k]="$COMMON $DEV -DOM_WF_LANES_PER_CU=3072"
   # r02: Sphere::hit without the divisions when both roots are provably rejected (default off:
