@@ -2,6 +2,8 @@
 (raytracingoneweekend_amd, HIP) and the oracle side (CPU restatement)."""
 import numpy as np
 
+F = np.float32
+
 
 def kitchen_sink(om, O):
     """Every primitive type of hits.rs:370-371, each constructor path used at least once."""
@@ -57,3 +59,84 @@ def compare_stats(got, exp, label=""):
                         f"depth={exp['avg_depth'][i]} bloom={exp['bloom'][i]:x}")
         msg = f"{label}: {nb}/{len(bad)} pixels differ\n" + "\n".join(rows)
     return nb, msg
+
+
+def compare_stats_nan_payload(got, exp, label=""):
+    """compare_stats, except that a NaN in `sum` only has to be a NaN on both sides: the sign
+    and mantissa bits of a NaN are not fixed across CPU and GPU (x86's default NaN carries the
+    sign bit, gfx950's does not).  Every other byte must match."""
+    g = got.copy()
+    e = exp.copy()
+    gn, en = np.isnan(g["sum"]), np.isnan(e["sum"])
+    both = gn & en
+    g["sum"][both] = 0.0
+    e["sum"][both] = 0.0
+    nb, msg = compare_stats(g, e, label)
+    mism = int((gn != en).any(axis=1).sum())
+    if mism and not nb:
+        nb, msg = mism, f"{label}: NaN-ness differs on {mism} pixels"
+    return nb, msg
+
+
+def tie_scene(om, O, duplicates=True):
+    """Ground + a 10x10 field of ellipsoids (every 5th followed by an exact duplicate with another
+    material: ties inside one BVH leaf) + a unit sphere at (4,1,0) added 10 times with 10
+    materials (degenerate centroids: the builder's median split deals the copies over several
+    leaves) + a cube twice + a triangle and a parallelogram from the same three points.
+    duplicates=False drops every later copy: the frame where the FIRST object would win."""
+    w, ow = om.HittableList.new(), O.World()
+    rng = np.random.default_rng(20260117)
+    palette = [("lambertian", (0.8, 0.3, 0.2), 0.0, 0.0), ("metal", (0.7, 0.8, 0.9), 0.1, 0.0),
+               ("dielectric", (0.0, 0.0, 0.0), 0.0, 1.5), ("lambertian", (0.1, 0.6, 0.2), 0.0, 0.0),
+               ("metal", (0.9, 0.6, 0.3), 0.4, 0.0)]
+
+    def mat(k):
+        kind, alb, fuzz, ior = palette[k % len(palette)]
+        if kind == "lambertian":
+            return om.Material.new_lambertian(alb), O.material(kind, alb)
+        if kind == "metal":
+            return om.Material.new_metal_fuzz(alb, fuzz), O.material(kind, alb, fuzz=fuzz)
+        return om.Material.new_dielectric(ior), O.material(kind, ior=ior)
+
+    m, m_ = mat(0)
+    w += om.Sphere.new_with_radius((0., -1000., 0.), 1000., m); ow.add_sphere_radius((0., -1000., 0.), 1000., m_)
+    k = 0
+    for a in range(-5, 5):
+        for b in range(-5, 5):
+            u = rng.random(6, dtype=F)
+            l2w = om.m4x4("TR", F(a) + F(0.9) * u[0], F(0.2), F(b) + F(0.9) * u[1]) \
+                ^ om.m4x4("RX", u[2] * F(6.2831855)) ^ om.m4x4("RY", u[3] * F(6.2831855)) \
+                ^ om.m4x4("SC", F(0.2) * (u[4] + F(1.)), F(0.2), F(0.2) * (u[5] + F(1.)))
+            copies = 2 if (duplicates and k % 5 == 0) else 1
+            for c in range(copies):
+                m, m_ = mat(k + 2 * c)
+                w += om.Sphere.new(l2w, m); ow.add_sphere(l2w.to_numpy(), m_)
+            k += 1
+    for c in range(10 if duplicates else 1):
+        m, m_ = mat(c)
+        w += om.Sphere.new_with_radius((4., 1., 0.), 1., m); ow.add_sphere_radius((4., 1., 0.), 1., m_)
+    l2w = om.m4x4("TR", 0., 1., 0.) ^ om.m4x4("RX", 0.5) ^ om.m4x4("RY", 0.9) ^ om.m4x4("SC", 1.2, 1.2, 1.2)
+    for c in range(2 if duplicates else 1):
+        m, m_ = mat(3 + c)
+        w += om.Cube.new(l2w, m); ow.add_cube(l2w.to_numpy(), m_)
+    p1, p2, p3 = (-4., 0.3, -1.), (-3.5, 2.2, -1.2), (-2.2, 0.5, 1.)
+    m, m_ = mat(1)
+    w += om.Triangle.new3points(p1, p2, p3, m); ow.add_triangle(p1, p2, p3, m_)
+    if duplicates:
+        m, m_ = mat(0)
+        w += om.Parallelogram.new3points(p1, p2, p3, m); ow.add_parallelogram(p1, p2, p3, m_)
+    return w, ow
+
+
+def nan_normal_world(om, O):
+    """A marched world whose box face sits at local |x| = 3 (marched.rs:25-44 -> NaN normals
+    there), next to a marched sphere and a marched ground (normals well defined)."""
+    w, ow = om.HittableList.new(), O.World()
+    lam = (om.Material.new_lambertian((0.7, 0.6, 0.5)), O.material("lambertian", (0.7, 0.6, 0.5)))
+    met = (om.Material.new_metal_fuzz((0.8, 0.8, 0.8), 0.2), O.material("metal", (0.8, 0.8, 0.8), fuzz=0.2))
+    die = (om.Material.new_dielectric(1.5), O.material("dielectric", ior=1.5))
+    w += om.MarchedSphere((0., -1000., 0.), 1000., lam[0]); ow.add_marched_sphere((0., -1000., 0.), 1000., lam[1])
+    w += om.MarchedBox((0., 0.6, 0.), (3., 0.6, 0.5), met[0]); ow.add_marched_box((0., 0.6, 0.), (3., 0.6, 0.5), met[1])
+    w += om.MarchedBox((0., 0.5, 2.2), (3., 0.5, 0.4), lam[0]); ow.add_marched_box((0., 0.5, 2.2), (3., 0.5, 0.4), lam[1])
+    w += om.MarchedSphere((4., 1., -1.5), 1., die[0]); ow.add_marched_sphere((4., 1., -1.5), 1., die[1])
+    return w, ow

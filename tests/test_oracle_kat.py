@@ -334,3 +334,43 @@ def test_exhausted_depth_colour_is_negative_zero(oracle):
     st, _ = _render_one(oracle, w, cam, depth=3)
     assert (st["sum"].view(np.uint32) == 0).all()                      # +0 bit patterns
     assert (st["color"] == 0).all() and (st["n"] == 2).all()
+
+
+def test_oracle_tie_scene_later_copy_wins(om, oracle):
+    """The oracle itself on the tie scene: a ray at the 10-copy sphere returns the LAST copy, one
+    at the shared triangle/parallelogram plane returns the parallelogram (hits.rs:274-285)."""
+    from scenes_common import tie_scene
+    _, ow = tie_scene(om, oracle)
+    c = ow.counts()
+    hit = ow.hit((13., 2., 3.), tuple(np.subtract((4., 1., 0.), (13., 2., 3.))))
+    assert hit is not None and hit[1] == c[0]              # the last sphere (obj id = gi + 1)
+    p1, p2, p3 = (np.array(p) for p in ((-4., 0.3, -1.), (-3.5, 2.2, -1.2), (-2.2, 0.5, 1.)))
+    n = np.cross(p2 - p1, p3 - p1)
+    n /= np.linalg.norm(n)
+    centroid = (p1 + p2 + p3) / 3
+    hit = ow.hit(tuple(centroid - 3 * n), tuple(n))      # from the side outside the ellipsoid field
+    para0 = c[0] + c[1] + c[2] + c[3]                      # type order: spheres, cubes, triangles, planes, parallelograms
+    assert hit is not None and hit[1] == para0 + 1
+
+def test_oracle_tie_scene_duplicates_decide_pixels(om, oracle):
+    """The oracle frames of the tie scene with and without the later copies differ in the winning
+    ids of many pixels, so the GPU tie tests (test_gpu_edge_cases.py) exercise real ties."""
+    from scenes_common import tie_scene
+    W, H, SPP = 32, 20, 1
+    _, ow = tie_scene(om, oracle)
+    _, ow1 = tie_scene(om, oracle, duplicates=False)
+    cam = oracle.default_camera(W / H)
+    a, _ = oracle.render(ow, cam, oracle.params(W, H, SPP, seed=29))
+    b, _ = oracle.render(ow1, cam, oracle.params(W, H, SPP, seed=29))
+    assert int((a["bloom"] != b["bloom"]).sum()) > W * H // 20
+
+
+def test_oracle_nan_normal_scene_reaches_nan(om, oracle):
+    """The marched box face at local |x| = 3 gives NaN normals (marched.rs:25-44), which reach
+    the pixels' running sums; the GPU test compares against exactly these frames."""
+    from scenes_common import nan_normal_world
+    W, H, SPP = 32, 20, 1
+    _, ow = nan_normal_world(om, oracle)
+    st, _ = oracle.render(ow, oracle.default_camera(W / H), oracle.params(W, H, SPP, seed=31, march_steps=256))
+    n_nan = int(np.isnan(st["sum"]).any(axis=1).sum())
+    assert 0 < n_nan < W * H
