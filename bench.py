@@ -90,14 +90,17 @@ BOUNCE_FAMILY = ("bounce0", "bounce", "tail")            # trace+shade launches 
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")          # C1; other configs: pmc_traffic_<config>.json
 
 
-def cpu_baseline(cfg, budget_s, lib="liboro.so"):
+def cpu_baseline(cfg, budget_s, lib="liboro.so", threads=0, dump=None):
     """The oracle (CPU restatement, `port`) on the host cores, in a child process
     (oracle/cpu_bench.py, which never touches the GPU): the reference's thread scheme on the
     config's frame for about `budget_s` seconds of full 1-spp passes.  `lib` picks the build
-    (liboro.so: -O3 default x86-64; liboro_v3.so: -O3 -march=x86-64-v3)."""
+    (liboro.so: -O3 default x86-64; liboro_v3.so: -O3 -march=x86-64-v3).  threads: 0 =
+    num_cpus::get() - 1 as main.rs:170 (the cgroup quota if set, else the affinity mask);
+    -1 = num_cpus::get()."""
     env = dict(os.environ, ORO_LIB=lib)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_bench.py"), "--config", cfg,
-                        "--budget", str(budget_s)], env=env, capture_output=True, text=True, timeout=600)
+                        "--budget", str(budget_s), "--threads", str(threads)] + (["--dump", dump] if dump else []),
+                       env=env, capture_output=True, text=True, timeout=600)
     if r.returncode != 0:
         raise RuntimeError(f"cpu baseline {cfg}/{lib} failed: {r.stderr[-2000:]}")
     return json.loads(r.stdout.strip().splitlines()[-1])
@@ -351,7 +354,9 @@ def main():
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, args.cpu_budget)
         cpu["second"] = cpu_baseline(args.config, args.cpu_budget, "liboro_v3.so")
+        cpu["all_cores"] = cpu_baseline(args.config, args.cpu_budget, threads=-1)   # nproc-1 and nproc
 
+    rccl = shard.rccl_library()       # the RCCL om_gather_frame ran on (torch's, by soname: DESIGN.md §6)
     if rank == 0:
         out = {
             "metric": "Msamples/s (W×H×spp/s) + achieved HBM GB/s, 1080p@512spp traced scene",
@@ -369,6 +374,7 @@ def main():
             "config": {"workload": workload(args.config, r), "width": r["W"], "height": r["H"],
                        "spp_per_step": r["spp_step"], "max_depth": r["depth"],
                        "parallelism": f"tile{world_size}", "gather": "RCCL send/recv (om_gather_frame)",
+                       "rccl_library": rccl[0], "rccl_version": rccl[1],
                        "kernel": args.kernel,
                        "pipeline": args.pipeline + (("->megakernel" if r["mega"] else "->wavefront")
                                                     if args.pipeline == "auto" else ""),
@@ -409,11 +415,19 @@ def run_c0(args, reps=20):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / reps
     got = frames[0].cpu().numpy()
+    same = all(torch.equal(b, frames[0]) for b in frames[1:])
     fz.close()
-    cpu = cpu_baseline("C0", 0.0)
+    import tempfile
+    with tempfile.TemporaryDirectory() as td:
+        dump = os.path.join(td, "c0_oracle.npy")
+        cpu = cpu_baseline("C0", 0.0, dump=dump)                        # the oracle renders the same frame
+        exp = np.load(dump, allow_pickle=False)
+    bad = int(np.any(got.reshape(-1, 40) != exp.view(np.uint8).reshape(-1, 40), axis=1).sum())
+    assert bad == 0, f"C0: {bad} pixels of the GPU frame differ from the oracle's"
     return {"metric": "Msamples/s", "value": round(W * H * cfg["spp"] / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 4),
             "workload": f"C0 S-traced {W}x{H}, {cfg['spp']} spp, depth {cfg['depth']} (whole frame per step, {reps} frames)",
             "frame_n_ok": bool((got.view(L.PIXEL_STATS_DTYPE)["n"] == cfg["spp"]).all()),
+            "frame_bit_exact_vs_oracle": bad == 0, "frames_identical": bool(same),
             "cpu_baseline": cpu, "gpu_over_cpu": round(W * H * cfg["spp"] / dt / 1e6 / cpu["value"], 1)}
 
 

@@ -332,6 +332,11 @@ om_status om_shard_assemble_host(uint32_t width, uint32_t height, uint32_t nrank
  * blocks until all ranks joined.  A comm is bound to ctx's device and is driven from one
  * host thread. */
 #define OM_COMM_ID_BYTES 128
+/* The RCCL library serving om_comm_* / om_multi_* in this process: its file (from the dynamic
+ * loader, NUL-terminated into path[path_bytes]) and its version (ncclGetVersion).  The library
+ * links /opt/rocm/lib's RCCL; a process that loaded another one first (PyTorch-ROCm ships its
+ * own, with its own HIP runtime) binds to that one by soname. */
+om_status om_rccl_library(char* path, uint32_t path_bytes, int32_t* version);
 typedef struct om_comm om_comm;
 om_status om_comm_unique_id(uint8_t id[OM_COMM_ID_BYTES]);
 om_status om_comm_init_rank(om_ctx* ctx, uint32_t nranks, uint32_t rank, const uint8_t id[OM_COMM_ID_BYTES],
@@ -363,16 +368,26 @@ int32_t om_multi_transport(const om_multi* m);      /* OM_TRANSPORT_*, or -1 for
 /* The ctx of one rank (kernel, pipeline, timing, counters ... apply per rank); owned by m. */
 om_ctx* om_multi_ctx(om_multi* m, uint32_t rank);
 om_status om_multi_upload_world(om_multi* m, const om_world* w);
-/* One progressive call over the whole frame, like om_render_device: dev_frame (W*H device
- * memory on devices[0]) is read and written in place.  Rank 0 deals the frame's shards to
- * the ranks, every rank renders its tiles on its own stream, and the shards come back to
- * dev_frame.  Asynchronous on `stream` (a stream of devices[0]; NULL = rank 0's ctx stream):
- * synchronising it covers the whole call. */
+/* One progressive call over the whole frame, like om_render_device on dev_frame (W*H device
+ * memory on devices[0]), with the ranks' shards RESIDENT on their GPUs between calls: the
+ * first call that sees dev_frame (or another pointer or size, or the first after
+ * om_multi_reset) cuts it into shards and deals them out; later calls only render, every rank
+ * its tiles on its own stream.  dev_frame is brought up to date by om_multi_gather, not by this
+ * call (the reference's one shared framebuffer without a per-pass copy, main.rs:192-214).
+ * Call om_multi_reset after writing dev_frame yourself.  Asynchronous on `stream` (a stream of
+ * devices[0]; NULL = rank 0's ctx stream). */
 om_status om_multi_render(om_multi* m, const om_camera* cam, const om_render_params* p, om_pixel_stats* dev_frame,
                           void* stream);
+/* The resident shards back into dev_frame (W*H device memory on devices[0]; normally the frame
+ * om_multi_render was given): one RCCL group (or device copies) into rank 0 plus the scatter.
+ * Ordered after every rank's last om_multi_render; asynchronous on `stream`. */
+om_status om_multi_gather(om_multi* m, om_pixel_stats* dev_frame, uint32_t width, uint32_t height, void* stream);
+/* Forget the resident frame: the next om_multi_render deals its frame out again. */
+void om_multi_reset(om_multi* m);
 /* Host framebuffer form (like om_render): `stats` (W*H, caller-owned host memory) is copied
- * to devices[0], rendered across the ranks and copied back; synchronous.  `counters`
- * (optional) sums every rank's work counters of this call. */
+ * to devices[0] and dealt out when the call sees this buffer first (as above; om_multi_reset
+ * after writing it yourself); every call renders across the ranks, gathers once and copies the
+ * frame back; synchronous.  `counters` (optional) sums every rank's work counters of this call. */
 om_status om_multi_render_host(om_multi* m, const om_camera* cam, const om_render_params* p, om_pixel_stats* stats,
                                om_counters* counters);
 const char* om_multi_last_error(const om_multi* m);

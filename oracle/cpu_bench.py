@@ -5,7 +5,7 @@ budget is spent, and prints one JSON object.  Which build is timed is chosen by 
 (liboro.so: -O3, default x86-64 target; liboro_v3.so: -O3 -march=x86-64-v3), so bench.py runs
 this as a subprocess once per build.
 
-    ORO_LIB=liboro_v3.so python oracle/cpu_bench.py --config C1 --budget 12 --threads 15
+    ORO_LIB=liboro_v3.so python oracle/cpu_bench.py --config C1 --budget 12 [--threads N]
 """
 import argparse
 import json
@@ -43,7 +43,33 @@ def cpu_model():
     return "unknown"
 
 
-def run(cfg, budget_s, threads, spp_total=64, seed=1):
+def cgroup_quota_cpus():
+    """The cgroup CPU quota in CPUs, rounded up (cgroup v2 cpu.max, else v1 cfs_quota/period),
+    or None when there is none."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            return max(1, -(-int(q) // int(per)))
+        return None
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return max(1, -(-q // per)) if q > 0 else None
+    except (OSError, ValueError):
+        return None
+
+
+def num_cpus():
+    """num_cpus::get() on Linux (num_cpus 1.x, what main.rs:170 calls): the cgroup CPU quota when
+    one is set, else the CPUs of the affinity mask.  -> (num_cpus, affinity count, quota or None)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_quota_cpus()
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def run(cfg, budget_s, threads, spp_total=64, seed=1, dump=None):
     """Full 1-spp passes of the config's frame (C3: a 1/64-area frame of the same scene and camera,
     since the oracle is brute force over 10k spheres and the per-sample cost does not depend on
     the resolution; C0: its whole 400x225x64 frame at depth 8)."""
@@ -61,8 +87,13 @@ def run(cfg, budget_s, threads, spp_total=64, seed=1):
         t_total += time.perf_counter() - t0
         done += ctr["samples"]
         passes += 1
+    if dump:
+        np.save(dump, stats, allow_pickle=False)           # the frame, for bench.py's C0 bit-exactness check
+    nc, aff, quota = num_cpus()
     return {"value": done / t_total / 1e6, "unit": "Msamples/s", "cores": threads, "kind": "port",
             "build": os.path.basename(O.LIB), "seconds": round(t_total, 3), "samples": int(done),
+            "num_cpus": nc, "affinity_cpus": aff, "cgroup_quota_cpus": quota,
+            "threads_rule": "num_cpus::get() - 1 (main.rs:170): the cgroup quota if set, else the affinity mask",
             "nproc": os.cpu_count(), "cpu_model": cpu_model(),
             "sample": f"{cfg} frame {w}x{h}, {passes} spp (full 1-spp passes), depth {depth}, {SCENES[cfg]}, "
                       f"{threads} threads ({os.path.basename(O.LIB)}), {t_total:.1f} s"}
@@ -72,7 +103,10 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C1", choices=list(SCENES))
     ap.add_argument("--budget", type=float, default=12.0)
-    ap.add_argument("--threads", type=int, default=0, help="0: num_cpus-1 as main.rs:170 (OMP_NUM_THREADS-1 if set)")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="0: num_cpus::get() - 1 as main.rs:170; -1: num_cpus::get() (the all-cores point)")
+    ap.add_argument("--dump", default=None, help="save the rendered Stats (.npy) here")
     a = ap.parse_args()
-    t = a.threads or max(1, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 2)) - 1)
-    print(json.dumps(run(a.config, a.budget, t)))
+    n = num_cpus()[0]
+    t = a.threads if a.threads > 0 else (n if a.threads < 0 else max(1, n - 1))
+    print(json.dumps(run(a.config, a.budget, t, dump=a.dump)))

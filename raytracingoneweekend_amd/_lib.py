@@ -78,7 +78,7 @@ EXPORTS = [
     "om_comm_destroy", "om_render_shard", "om_gather_frame", "om_scatter_frame", "om_multi_create",
     "om_multi_destroy", "om_multi_transport", "om_multi_ctx", "om_multi_upload_world", "om_multi_render",
     "om_multi_last_error", "om_progress", "om_reset_progress", "om_host_register", "om_host_unregister",
-    "om_multi_render_host",
+    "om_multi_render_host", "om_multi_gather", "om_multi_reset", "om_rccl_library",
 ]
 OM_COMM_ID_BYTES = 128
 OM_TRANSPORT_RCCL, OM_TRANSPORT_LOCAL = 0, 1
@@ -186,6 +186,9 @@ def _load():
         "om_host_register": (st, [vp, C.c_size_t]),
         "om_host_unregister": (st, [vp]),
         "om_multi_render_host": (st, [vp, C.POINTER(om_camera), C.POINTER(om_render_params), vp, C.POINTER(om_counters)]),
+        "om_multi_gather": (st, [vp, vp, C.c_uint32, C.c_uint32, vp]),
+        "om_multi_reset": (None, [vp]),
+        "om_rccl_library": (st, [C.c_char_p, C.c_uint32, C.POINTER(C.c_int32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

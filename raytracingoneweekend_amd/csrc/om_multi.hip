@@ -12,10 +12,12 @@
 //   pixel, HBM-bound, coalesced 8-B words).
 // The 332-MB C4 frame puts 41.5 MB on each peer's own xGMI link into rank 0 (~0.3 ms at
 // ~150 GB/s), against seconds of rendering.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -62,6 +64,14 @@ hipError_t launch_move(bool to_frame, const void* src, const uint32_t* list, uin
     return hipGetLastError();
 }
 
+// Test hook (tests/test_multi_gpu.py): OM_DEBUG_FAIL_ALLOC=<bytes> makes every DBuf allocation
+// of at least that many bytes fail as if the device were out of memory, so the error and retry
+// paths of the shard bookkeeping can be exercised without exhausting 288 GB of HBM.
+bool debug_fail_alloc(size_t bytes) {
+    const char* v = std::getenv("OM_DEBUG_FAIL_ALLOC");
+    return v && *v && bytes >= (size_t)std::strtoull(v, nullptr, 10);
+}
+
 struct DBuf {
     void* p = nullptr;
     size_t n = 0;
@@ -69,6 +79,7 @@ struct DBuf {
     hipError_t ensure(int device, size_t bytes) {
         if (p && n >= bytes && dev == device) return hipSuccess;
         release();
+        if (debug_fail_alloc(bytes)) return hipErrorOutOfMemory;
         hipError_t e = hipSetDevice(device);
         if (e == hipSuccess) e = hipMalloc(&p, std::max<size_t>(bytes, 16));
         if (e != hipSuccess) { p = nullptr; return e; }
@@ -140,6 +151,22 @@ om_status check_frame(om_ctx* ctx, uint32_t W, uint32_t H) {
 }  // namespace
 
 extern "C" {
+
+om_status om_rccl_library(char* path, uint32_t path_bytes, int32_t* version) {
+    if (path && path_bytes) {
+        Dl_info info{};
+        const char* f = dladdr((void*)&ncclGetUniqueId, &info) && info.dli_fname ? info.dli_fname : "";
+        std::strncpy(path, f, path_bytes - 1);
+        path[path_bytes - 1] = '\0';
+    }
+    if (version) {
+        int v = 0;
+        const ncclResult_t r = ncclGetVersion(&v);
+        if (r != ncclSuccess) return omi::global_error(OM_ERR_DEVICE, nccl_msg("ncclGetVersion", r));
+        *version = v;
+    }
+    return OM_OK;
+}
 
 om_status om_comm_unique_id(uint8_t id[OM_COMM_ID_BYTES]) {
     static_assert(sizeof(ncclUniqueId) == OM_COMM_ID_BYTES, "ncclUniqueId size");
@@ -253,6 +280,10 @@ om_status om_scatter_frame(om_comm* c, const om_pixel_stats* dev_frame, uint32_t
 // ---------------------------------------------------------------------------
 // one process, several GPUs
 // ---------------------------------------------------------------------------
+// The shards stay resident on their GPUs across progressive calls, as the reference's render
+// threads keep writing one shared framebuffer with no per-pass copy (main.rs:192-214): a
+// frame is dealt out once, when om_multi_render first sees it (its device pointer and size),
+// and comes back only when om_multi_gather asks for it.
 struct om_multi {
     std::vector<om_ctx*> ctx;
     std::vector<int> dev;
@@ -262,8 +293,14 @@ struct om_multi {
     std::vector<DBuf> list;             // per rank r > 0: its list on its device
     std::vector<DBuf> shard;            // per rank: its shard on its device (HBM-resident)
     std::vector<DBuf> staging;          // per rank r > 0: its shard's image on devices[0]
-    std::vector<hipEvent_t> ev;         // [0] on devices[0]: frame cut; [r]: rank r done
+    std::vector<hipEvent_t> ev;         // [0] on devices[0]: frame cut / gather done; [r]: rank r's stream
+    bool ev0_live = false;              // ev[0] has been recorded (the ranks' streams wait on it)
+    hipEvent_t done0 = nullptr;         // on devices[0]: rank 0's last render
+    const void* bound = nullptr;        // the device frame whose shards are resident
+    uint32_t bw = 0, bh = 0;
     DBuf host_frame;                    // om_multi_render_host: the frame on devices[0]
+    const void* host_bound = nullptr;   // the host framebuffer host_frame mirrors
+    size_t host_bytes = 0;
     std::string err;
 };
 
@@ -280,9 +317,8 @@ om_status merr(om_multi* m, om_status code, const std::string& msg) {
         if (e_ != hipSuccess) return merr(m, OM_ERR_DEVICE, std::string(#call ": ") + hipGetErrorString(e_)); \
     } while (0)
 
-om_status multi_lists(om_multi* m, uint32_t W, uint32_t H) {
+om_status multi_lists_build(om_multi* m, uint32_t W, uint32_t H) {
     const uint32_t N = (uint32_t)m->ctx.size();
-    if (m->deal.valid(W, H, N)) return OM_OK;
     OM_MHIP(m, m->deal.build(W, H, N, m->dev[0]));
     std::vector<uint32_t> lst;
     const size_t cap_b = (size_t)m->deal.cap * sizeof(om_pixel_stats);
@@ -298,6 +334,68 @@ om_status multi_lists(om_multi* m, uint32_t W, uint32_t H) {
     return OM_OK;
 }
 
+// The deal's lists, shards and staging buffers for (W, H).  The deal counts as built only once
+// every per-rank buffer is in place: a failure part-way (an allocation, a copy) releases the
+// rank-major table, so the next call rebuilds everything instead of launching on missing or
+// undersized buffers.  A new deal forgets the resident frame.
+om_status multi_lists(om_multi* m, uint32_t W, uint32_t H) {
+    if (m->deal.valid(W, H, (uint32_t)m->ctx.size())) return OM_OK;
+    m->bound = nullptr;
+    const om_status s = multi_lists_build(m, W, H);
+    if (s != OM_OK) m->deal.all.release();
+    return s;
+}
+
+std::vector<hipStream_t> rank_streams(om_multi* m, void* stream) {
+    std::vector<hipStream_t> st(m->ctx.size());
+    for (size_t r = 0; r < st.size(); ++r) st[r] = omi::ctx_stream(m->ctx[r]);
+    if (stream) st[0] = (hipStream_t)stream;
+    return st;
+}
+
+// ev[0] on st[0], and every rank's stream waits on it.
+om_status fence_from_root(om_multi* m, const std::vector<hipStream_t>& st) {
+    OM_MHIP(m, hipSetDevice(m->dev[0]));
+    OM_MHIP(m, hipEventRecord(m->ev[0], st[0]));
+    m->ev0_live = true;
+    for (size_t r = 1; r < st.size(); ++r) {
+        OM_MHIP(m, hipSetDevice(m->dev[r]));
+        OM_MHIP(m, hipStreamWaitEvent(st[r], m->ev[0], 0));
+    }
+    return OM_OK;
+}
+
+// Rank 0 cuts dev_frame into the shards (its own in place, the others' into staging) and deals
+// them out: the frame becomes the resident one.
+om_status deal_frame(om_multi* m, const om_pixel_stats* dev_frame, const std::vector<hipStream_t>& st) {
+    const uint32_t N = (uint32_t)m->ctx.size();
+    const Deal& D = m->deal;
+    OM_MHIP(m, hipSetDevice(m->dev[0]));
+    for (uint32_t r = 0; r < N; ++r)
+        OM_MHIP(m, launch_move(false, dev_frame, D.list(r), D.count[r], r ? m->staging[r].p : m->shard[0].p, st[0]));
+    if (m->transport == OM_TRANSPORT_RCCL && N > 1) {
+        ncclResult_t e = ncclGroupStart();
+        for (uint32_t r = 1; e == ncclSuccess && r < N; ++r) {
+            const size_t b = (size_t)D.count[r] * sizeof(om_pixel_stats);
+            if (!b) continue;
+            e = ncclSend(m->staging[r].p, b, ncclUint8, (int)r, m->nc[0], st[0]);
+            if (e == ncclSuccess) e = ncclRecv(m->shard[r].p, b, ncclUint8, 0, m->nc[r], st[r]);
+        }
+        const ncclResult_t e2 = ncclGroupEnd();
+        if (e != ncclSuccess || e2 != ncclSuccess) return merr(m, OM_ERR_DEVICE, nccl_msg("om_multi deal", e != ncclSuccess ? e : e2));
+    } else {
+        for (uint32_t r = 1; r < N; ++r)
+            if (D.count[r])
+                OM_MHIP(m, hipMemcpyPeerAsync(m->shard[r].p, m->dev[r], m->staging[r].p, m->dev[0],
+                                              (size_t)D.count[r] * sizeof(om_pixel_stats), st[0]));
+    }
+    return fence_from_root(m, st);
+}
+
+bool frame_bound(const om_multi* m, const void* f, uint32_t W, uint32_t H) {
+    return m->bound && m->bound == f && m->bw == W && m->bh == H;
+}
+
 }  // namespace
 
 extern "C" {
@@ -311,6 +409,10 @@ om_status om_multi_create(const int32_t* devices, uint32_t n, om_multi** out) {
     m->ctx.assign(n, nullptr);
     m->list.resize(n); m->shard.resize(n); m->staging.resize(n);
     m->ev.assign(n, nullptr);
+    if (hipSetDevice(devices[0]) != hipSuccess || hipEventCreateWithFlags(&m->done0, hipEventDisableTiming) != hipSuccess) {
+        om_multi_destroy(m);
+        return merr(nullptr, OM_ERR_DEVICE, "om_multi_create: event creation failed");
+    }
     for (uint32_t r = 0; r < n; ++r) {
         om_status s = om_create(devices[r], &m->ctx[r]);
         if (s != OM_OK) { const std::string msg = om_last_error(nullptr); om_multi_destroy(m); return merr(nullptr, s, msg); }
@@ -350,6 +452,7 @@ void om_multi_destroy(om_multi* m) {
     m->host_frame.release();
     for (size_t r = 0; r < m->ev.size(); ++r)
         if (m->ev[r]) { (void)hipSetDevice(m->dev[r]); (void)hipEventDestroy(m->ev[r]); }
+    if (m->done0) { (void)hipSetDevice(m->dev[0]); (void)hipEventDestroy(m->done0); }
     for (auto c : m->ctx) om_destroy(c);
     delete m;
 }
@@ -376,72 +479,75 @@ om_status om_multi_render(om_multi* m, const om_camera* cam, const om_render_par
     const uint32_t N = (uint32_t)m->ctx.size();
     om_status s = multi_lists(m, p->width, p->height);
     if (s) return s;
-    const Deal& D = m->deal;
-    std::vector<hipStream_t> st(N);
-    for (uint32_t r = 0; r < N; ++r) st[r] = omi::ctx_stream(m->ctx[r]);
-    if (stream) st[0] = (hipStream_t)stream;
-    // 1. rank 0 cuts the caller's frame into shards (its own in place, the others' into staging)
-    OM_MHIP(m, hipSetDevice(m->dev[0]));
-    for (uint32_t r = 0; r < N; ++r)
-        OM_MHIP(m, launch_move(false, dev_frame, D.list(r), D.count[r], r ? m->staging[r].p : m->shard[0].p, st[0]));
-    // 2. deal them out
-    if (m->transport == OM_TRANSPORT_RCCL && N > 1) {
-        ncclResult_t e = ncclGroupStart();
-        for (uint32_t r = 1; e == ncclSuccess && r < N; ++r) {
-            const size_t b = (size_t)D.count[r] * sizeof(om_pixel_stats);
-            if (!b) continue;
-            e = ncclSend(m->staging[r].p, b, ncclUint8, (int)r, m->nc[0], st[0]);
-            if (e == ncclSuccess) e = ncclRecv(m->shard[r].p, b, ncclUint8, 0, m->nc[r], st[r]);
-        }
-        const ncclResult_t e2 = ncclGroupEnd();
-        if (e != ncclSuccess || e2 != ncclSuccess) return merr(m, OM_ERR_DEVICE, nccl_msg("om_multi_render deal", e != ncclSuccess ? e : e2));
-    } else if (N > 1) {
-        for (uint32_t r = 1; r < N; ++r)
-            if (D.count[r])
-                OM_MHIP(m, hipMemcpyPeerAsync(m->shard[r].p, m->dev[r], m->staging[r].p, m->dev[0],
-                                              (size_t)D.count[r] * sizeof(om_pixel_stats), st[0]));
-        OM_MHIP(m, hipEventRecord(m->ev[0], st[0]));
+    const std::vector<hipStream_t> st = rank_streams(m, stream);
+    if (!frame_bound(m, dev_frame, p->width, p->height)) {
+        // a new frame (first use, another buffer or size, or after om_multi_reset): deal it out
+        m->bound = nullptr;
+        if ((s = deal_frame(m, dev_frame, st))) return s;
+        m->bound = dev_frame; m->bw = p->width; m->bh = p->height;
+    } else if (m->ev0_live) {
+        // resident shards: the ranks start after rank 0's last deal or gather (which read them)
         for (uint32_t r = 1; r < N; ++r) {
             OM_MHIP(m, hipSetDevice(m->dev[r]));
             OM_MHIP(m, hipStreamWaitEvent(st[r], m->ev[0], 0));
         }
     }
-    // 3. every rank renders its tiles on its own stream (all devices at once)
+    // every rank renders its tiles into its resident shard on its own stream (all devices at once)
+    const Deal& D = m->deal;
     for (uint32_t r = 0; r < N; ++r) {
-        if (!D.count[r]) continue;
-        const uint32_t* lst = r ? (const uint32_t*)m->list[r].p : D.list(0);
-        s = om_render_device_pixels(m->ctx[r], cam, p, (om_pixel_stats*)m->shard[r].p, lst, D.count[r], st[r]);
-        if (s != OM_OK) return merr(m, s, std::string("rank ") + std::to_string(r) + ": " + om_last_error(m->ctx[r]));
+        if (D.count[r]) {
+            const uint32_t* lst = r ? (const uint32_t*)m->list[r].p : D.list(0);
+            s = om_render_device_pixels(m->ctx[r], cam, p, (om_pixel_stats*)m->shard[r].p, lst, D.count[r], st[r]);
+            if (s != OM_OK) return merr(m, s, std::string("rank ") + std::to_string(r) + ": " + om_last_error(m->ctx[r]));
+        }
+        OM_MHIP(m, hipSetDevice(m->dev[r]));
+        OM_MHIP(m, hipEventRecord(r ? m->ev[r] : m->done0, st[r]));
     }
-    // 4. shards back to rank 0
+    return OM_OK;
+}
+
+om_status om_multi_gather(om_multi* m, om_pixel_stats* dev_frame, uint32_t W, uint32_t H, void* stream) {
+    if (!m || !dev_frame) return merr(m, OM_ERR_INVALID, "om_multi_gather: null argument");
+    if (!m->bound || m->bw != W || m->bh != H || !m->deal.valid(W, H, (uint32_t)m->ctx.size()))
+        return merr(m, OM_ERR_INVALID, "om_multi_gather: no resident frame of this size (om_multi_render first)");
+    const uint32_t N = (uint32_t)m->ctx.size();
+    const Deal& D = m->deal;
+    const std::vector<hipStream_t> st = rank_streams(m, stream);
+    OM_MHIP(m, hipSetDevice(m->dev[0]));
+    OM_MHIP(m, hipStreamWaitEvent(st[0], m->done0, 0));                // rank 0's last render (any stream)
     if (m->transport == OM_TRANSPORT_RCCL && N > 1) {
         ncclResult_t e = ncclGroupStart();
         for (uint32_t r = 1; e == ncclSuccess && r < N; ++r) {
             const size_t b = (size_t)D.count[r] * sizeof(om_pixel_stats);
             if (!b) continue;
-            e = ncclSend(m->shard[r].p, b, ncclUint8, 0, m->nc[r], st[r]);
+            e = ncclSend(m->shard[r].p, b, ncclUint8, 0, m->nc[r], st[r]);   // after rank r's render on st[r]
             if (e == ncclSuccess) e = ncclRecv(m->staging[r].p, b, ncclUint8, (int)r, m->nc[0], st[0]);
         }
         const ncclResult_t e2 = ncclGroupEnd();
-        if (e != ncclSuccess || e2 != ncclSuccess) return merr(m, OM_ERR_DEVICE, nccl_msg("om_multi_render gather", e != ncclSuccess ? e : e2));
+        if (e != ncclSuccess || e2 != ncclSuccess) return merr(m, OM_ERR_DEVICE, nccl_msg("om_multi_gather", e != ncclSuccess ? e : e2));
     } else if (N > 1) {
-        for (uint32_t r = 1; r < N; ++r) {
-            OM_MHIP(m, hipSetDevice(m->dev[r]));
-            OM_MHIP(m, hipEventRecord(m->ev[r], st[r]));
-        }
         OM_MHIP(m, hipSetDevice(m->dev[0]));
         for (uint32_t r = 1; r < N; ++r) {
-            OM_MHIP(m, hipStreamWaitEvent(st[0], m->ev[r], 0));
+            OM_MHIP(m, hipStreamWaitEvent(st[0], m->ev[r], 0));       // rank r's last render
             if (D.count[r])
                 OM_MHIP(m, hipMemcpyPeerAsync(m->staging[r].p, m->dev[0], m->shard[r].p, m->dev[r],
                                               (size_t)D.count[r] * sizeof(om_pixel_stats), st[0]));
         }
     }
-    // 5. rank 0 puts every shard back into the frame
+    // rank 0 puts every shard into the frame
     OM_MHIP(m, hipSetDevice(m->dev[0]));
     for (uint32_t r = 0; r < N; ++r)
         OM_MHIP(m, launch_move(true, r ? m->staging[r].p : m->shard[0].p, D.list(r), D.count[r], dev_frame, st[0]));
+    // the next render call's ranks overwrite their shards only after this read them
+    OM_MHIP(m, hipEventRecord(m->ev[0], st[0]));
+    m->ev0_live = true;
     return OM_OK;
+}
+
+void om_multi_reset(om_multi* m) {
+    if (!m) return;
+    m->bound = nullptr;
+    m->host_bound = nullptr;
 }
 
 om_status om_multi_render_host(om_multi* m, const om_camera* cam, const om_render_params* p, om_pixel_stats* stats,
@@ -450,16 +556,23 @@ om_status om_multi_render_host(om_multi* m, const om_camera* cam, const om_rende
     if (p->width == 0 || p->height == 0 || (uint64_t)p->width * p->height > (1ull << 31))
         return merr(m, OM_ERR_INVALID, "om_multi_render_host: width/height must be > 0");
     const size_t bytes = (size_t)p->width * p->height * sizeof(om_pixel_stats);
-    OM_MHIP(m, m->host_frame.ensure(m->dev[0], bytes));
     hipStream_t st = omi::ctx_stream(m->ctx[0]);
     for (auto c : m->ctx) {
         const om_status s = om_reset_counters(c, nullptr);
         if (s != OM_OK) return merr(m, s, om_last_error(c));
     }
     OM_MHIP(m, hipSetDevice(m->dev[0]));
-    OM_MHIP(m, hipMemcpyAsync(m->host_frame.p, stats, bytes, hipMemcpyHostToDevice, st));
+    if (m->host_bound != stats || m->host_bytes != bytes) {
+        // a new host framebuffer: mirror it on devices[0] and deal it out (first call only)
+        m->host_bound = nullptr;
+        m->bound = nullptr;
+        OM_MHIP(m, m->host_frame.ensure(m->dev[0], bytes));
+        OM_MHIP(m, hipMemcpyAsync(m->host_frame.p, stats, bytes, hipMemcpyHostToDevice, st));
+        m->host_bound = stats; m->host_bytes = bytes;
+    }
     om_status s = om_multi_render(m, cam, p, (om_pixel_stats*)m->host_frame.p, st);
-    if (s != OM_OK) return s;
+    if (s == OM_OK) s = om_multi_gather(m, (om_pixel_stats*)m->host_frame.p, p->width, p->height, st);
+    if (s != OM_OK) { m->host_bound = nullptr; return s; }
     OM_MHIP(m, hipSetDevice(m->dev[0]));
     OM_MHIP(m, hipMemcpyAsync(stats, m->host_frame.p, bytes, hipMemcpyDeviceToHost, st));
     OM_MHIP(m, hipStreamSynchronize(st));

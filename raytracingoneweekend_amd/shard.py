@@ -61,6 +61,14 @@ def _stdout_to_stderr():
         os.close(saved)
 
 
+def rccl_library():
+    """(path, version) of the RCCL library serving om_comm_* / om_multi_* in this process."""
+    buf = C.create_string_buffer(4096)
+    v = C.c_int32()
+    check(lib.om_rccl_library(buf, len(buf), C.byref(v)))
+    return buf.value.decode(), v.value
+
+
 def unique_id():
     """om_comm_unique_id: the 128 bytes rank 0 hands to every rank before Comm()."""
     buf = (C.c_uint8 * L.OM_COMM_ID_BYTES)()
@@ -131,9 +139,33 @@ class MultiFrame:
     def ctx(self, rank):
         return C.c_void_p(lib.om_multi_ctx(self._m, rank))
 
+    @staticmethod
+    def _stream(stream):
+        """The caller's stream; by default torch's current one, so the calls are ordered after the
+        work that produced dev_frame.  torch's legacy default stream has the NULL handle, which
+        the C-ABI reads as "the ctx's own stream" (not ordered with it): synchronise instead."""
+        if stream is not None:
+            return stream
+        import torch
+        s = torch.cuda.current_stream().cuda_stream
+        if not s:
+            torch.cuda.synchronize()
+        return s or None
+
     def render(self, cam, params, dev_frame_ptr, stream=None):
+        """One progressive call into the ranks' resident shards (om_multi_render); the first call
+        on a frame deals it out.  dev_frame is brought up to date by gather()."""
         self._check(lib.om_multi_render(self._m, C.byref(cam.raw), C.byref(params), C.c_void_p(dev_frame_ptr),
-                                        C.c_void_p(stream)))
+                                        C.c_void_p(self._stream(stream))))
+
+    def gather(self, dev_frame_ptr, width, height, stream=None):
+        """The resident shards back into dev_frame (om_multi_gather)."""
+        self._check(lib.om_multi_gather(self._m, C.c_void_p(dev_frame_ptr), int(width), int(height),
+                                        C.c_void_p(self._stream(stream))))
+
+    def reset(self):
+        """Forget the resident frame (after writing dev_frame yourself)."""
+        lib.om_multi_reset(self._m)
 
     def close(self):
         if getattr(self, "_m", None) and self._m.value:

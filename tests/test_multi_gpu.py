@@ -15,13 +15,14 @@ pytestmark = pytest.mark.gpu
 W4K, H4K = 3840, 2160          # BASELINE.json configs[4] (C4)
 
 
-def _full_frame(om, world, cam, W, H, spp, calls, seed):
-    """Single-device reference: one ctx, om_render_device over the whole frame."""
+def _full_frame(om, world, cam, W, H, spp, calls, seed, spp_total=None):
+    """Single-device reference: one ctx, `calls` om_render_device calls of spp // calls samples
+    (of spp_total, default spp: the jitter table's size) over the whole frame."""
     import torch
     from raytracingoneweekend_amd import _lib as L
     fz = world.freeze(cam)
     frame = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
-    p = om.make_params(50, 0.001, 100.0, spp, W, H, sample_count=spp // calls, seed=seed)
+    p = om.make_params(50, 0.001, 100.0, spp_total or spp, W, H, sample_count=spp // calls, seed=seed)
     for _ in range(calls):
         L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(frame.data_ptr()), None), fz.ctx)
     torch.cuda.synchronize()
@@ -29,36 +30,105 @@ def _full_frame(om, world, cam, W, H, spp, calls, seed):
     return frame
 
 
-def _window_vs_oracle(oracle, frame_u8, W, H, spp, seed, x0, y0, size=24):
+def _window_vs_oracle(oracle, frame_u8, W, H, spp, seed, x0, y0, size=24, sample_count=None):
     pix = np.array([(y0 + j) * W + x0 + i for j in range(size) for i in range(size)], dtype=np.uint32)
     exp = oracle.render_pixels(oracle.random_scene(0x5EED), oracle.default_camera(W / H),
-                               oracle.params(W, H, spp, seed=seed), pix)
+                               oracle.params(W, H, spp, sample_count=sample_count, seed=seed), pix)
     got = frame_u8.view(np.uint8).reshape(W * H, 40)[pix].copy().view(oracle.PIXEL_STATS_DTYPE).reshape(-1)
     return compare_stats(got, exp, f"window {x0},{y0}")
 
 
 @pytest.mark.parametrize("nranks", [2, 3, 8])
 def test_multi_local_ranks_4k_frame_bit_identical(om, oracle, nranks):
-    """om_multi over `nranks` logical ranks on device 0 (OM_TRANSPORT_LOCAL): two progressive
-    calls of C4's 4K frame (the second one deals a partly rendered frame back out) == one ctx."""
+    """om_multi over `nranks` logical ranks on device 0 (OM_TRANSPORT_LOCAL): C4's 4K frame dealt
+    out once, three progressive calls into the ranks' resident shards, ONE gather == one ctx.
+    Then a second frame buffer already holding those samples is dealt out (a frame rendered
+    elsewhere), one more call and gather == one ctx at the higher sample count."""
     import torch
     from raytracingoneweekend_amd import shard
     world = om.random_scene(0x5EED)
     cam = om.default_camera(W4K / H4K)
-    spp, seed = 2, 41
-    ref = _full_frame(om, world, cam, W4K, H4K, spp, 2, seed)
+    spp, seed = 3, 41
+    ref = _full_frame(om, world, cam, W4K, H4K, spp, 3, seed, spp_total=spp + 1)
     mf = shard.MultiFrame([0] * nranks, world)
     assert mf.transport == "local"
+    s = torch.cuda.Stream()
     frame = torch.zeros(W4K * H4K * 40, dtype=torch.uint8, device="cuda")
-    p = om.make_params(50, 0.001, 100.0, spp, W4K, H4K, sample_count=1, seed=seed)
-    for _ in range(2):
-        mf.render(cam, p, frame.data_ptr())
     torch.cuda.synchronize()
+    p = om.make_params(50, 0.001, 100.0, spp + 1, W4K, H4K, sample_count=1, seed=seed)
+    for _ in range(spp):
+        mf.render(cam, p, frame.data_ptr(), s.cuda_stream)
+    mf.gather(frame.data_ptr(), W4K, H4K, s.cuda_stream)
+    s.synchronize()
     assert torch.equal(frame, ref), f"{int((frame != ref).view(-1, 40).any(1).sum())} pixels differ"
     host = frame.cpu().numpy()
     assert int(host.view(om.PIXEL_STATS_DTYPE)["n"].min()) == spp
-    nb, msg = _window_vs_oracle(oracle, host, W4K, H4K, spp, seed, 1800, 1000)
+    nb, msg = _window_vs_oracle(oracle, host, W4K, H4K, spp + 1, seed, 1800, 1000, sample_count=spp)
     assert nb == 0, msg
+    # a second buffer (a frame rendered elsewhere): dealt out on first sight
+    ref4 = _full_frame(om, world, cam, W4K, H4K, spp + 1, spp + 1, seed)
+    frame2 = frame.clone()
+    torch.cuda.synchronize()
+    mf.render(cam, p, frame2.data_ptr(), s.cuda_stream)
+    mf.gather(frame2.data_ptr(), W4K, H4K, s.cuda_stream)
+    s.synchronize()
+    assert torch.equal(frame2, ref4)
+    mf.close()
+
+
+def test_multi_gather_stale_frame_and_reset(om):
+    """The frame only changes on gather; om_multi_reset re-deals a frame the caller rewrote."""
+    import torch
+    from raytracingoneweekend_amd import shard
+    W, H, seed = 200, 120, 44
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    mf = shard.MultiFrame([0, 0, 0], world)
+    frame = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
+    p = om.make_params(50, 0.001, 100.0, 4, W, H, sample_count=2, seed=seed)
+    mf.render(cam, p, frame.data_ptr())
+    torch.cuda.synchronize()
+    assert not frame.any(), "om_multi_render must not write the frame"
+    mf.gather(frame.data_ptr(), W, H)
+    torch.cuda.synchronize()
+    first = frame.clone()
+    frame.zero_()                                   # the caller restarts the frame ...
+    mf.reset()                                      # ... and says so
+    mf.render(cam, p, frame.data_ptr())
+    mf.gather(frame.data_ptr(), W, H)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, first)
+    with pytest.raises(Exception, match="no resident frame"):
+        mf.gather(frame.data_ptr(), W + 8, H)
+    mf.close()
+
+
+def test_multi_failed_allocation_then_retry(om, monkeypatch):
+    """a shard allocation that fails part-way through the deal's bookkeeping returns
+    an error and leaves no half-built deal behind; the retried call rebuilds it and renders the
+    same frame as one ctx (OM_DEBUG_FAIL_ALLOC: every shard-buffer allocation of >= N bytes
+    fails, om_multi.hip)."""
+    import torch
+    from raytracingoneweekend_amd import _lib as L
+    from raytracingoneweekend_amd import shard
+    W, H, spp, seed = W4K, H4K, 1, 45
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    ref = _full_frame(om, world, cam, W, H, spp, 1, seed)
+    mf = shard.MultiFrame([0, 0, 0], world)
+    frame = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    p = om.make_params(50, 0.001, 100.0, spp, W, H, seed=seed)
+    # the rank-major list table (33 MB) fits, every shard (110 MB) fails
+    monkeypatch.setenv("OM_DEBUG_FAIL_ALLOC", str(64 << 20))
+    for _ in range(2):
+        with pytest.raises(L.OmError, match="out of memory|ensure"):
+            mf.render(cam, p, frame.data_ptr())
+    monkeypatch.delenv("OM_DEBUG_FAIL_ALLOC")
+    mf.render(cam, p, frame.data_ptr())
+    mf.gather(frame.data_ptr(), W, H)
+    torch.cuda.synchronize()
+    assert torch.equal(frame, ref)
     mf.close()
 
 
@@ -74,9 +144,17 @@ def test_multi_rccl_transport_one_device(om):
     assert mf.transport == "rccl"
     frame = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
     mf.render(cam, om.make_params(50, 0.001, 100.0, spp, W, H, seed=seed), frame.data_ptr())
+    mf.gather(frame.data_ptr(), W, H)
     torch.cuda.synchronize()
     assert torch.equal(frame, ref)
     mf.close()
+
+
+def test_rccl_library_is_reported(om):
+    """om_rccl_library names the RCCL the comm paths run on (bench.py records it in the line)."""
+    from raytracingoneweekend_amd import shard
+    path, version = shard.rccl_library()
+    assert "rccl" in path and version >= 20000
 
 
 def test_comm_rank_render_gather_scatter_through_rccl(om, oracle):
