@@ -220,10 +220,13 @@ om_status om_reset_counters(om_ctx* ctx, void* stream);
  * log thread and display poll while the render threads run (main.rs:151-168, 371-377).
  * om_progress returns a host word the library keeps pinned; every later render call on ctx
  * adds its credited samples to it (each sample taken, plus a retiring pixel's untaken ones in
- * adaptive calls) as each batch of the call is accumulated, so it advances while a call runs.
+ * adaptive calls).  The wavefront pipeline adds each batch as it is accumulated, so the word
+ * advances while a call runs; the megakernel adds the whole call when its one launch ends.
  * Any host thread may read it without synchronising; it only grows.  After the call's stream
- * is synchronised it has grown by exactly the call's om_counters.credited.  om_reset_progress
- * zeroes it (synchronises the device).  NULL on error. */
+ * is synchronised it has grown by the call's credited samples; with counting on (the
+ * default, om_set_counting) that is exactly the call's om_counters.credited (with counting
+ * off the counters stay 0 and only this word advances).  om_reset_progress zeroes it
+ * (synchronises the device).  NULL on error. */
 const volatile uint64_t* om_progress(om_ctx* ctx);
 om_status om_reset_progress(om_ctx* ctx);
 /* Work counting on (default) / off.  Off selects kernel builds with the counters

@@ -340,16 +340,23 @@ class PixelsBox:
 
     def pin(self):
         """Page-lock the framebuffer (om_host_register) so render()'s copies run as DMA; kept
-        until the box dies.  Done by render() on first use (needs a HIP device)."""
+        until the box dies or `pixels` is replaced.  Best effort, like the C++ render(): a
+        refused registration (memlock limit, an already registered buffer) leaves the buffer
+        pageable, and the copies still work.  Done by render() on first use (needs a HIP device)."""
+        if self._pinned is not None and self._pinned is not self.pixels:
+            self.unpin()                                   # `pixels` was replaced: release the old one
         if self._pinned is None and self.pixels.nbytes:
-            check(lib.om_host_register(self.pixels.ctypes.data, self.pixels.nbytes))
-            self._pinned = self.pixels.ctypes.data
+            if lib.om_host_register(self.pixels.ctypes.data, self.pixels.nbytes) == L.OM_OK:
+                self._pinned = self.pixels                 # a reference: the array cannot be freed while registered
         return self
 
-    def __del__(self):
-        if getattr(self, "_pinned", None):
-            lib.om_host_unregister(self._pinned)
+    def unpin(self):
+        if getattr(self, "_pinned", None) is not None:
+            lib.om_host_unregister(self._pinned.ctypes.data)
             self._pinned = None
+
+    def __del__(self):
+        self.unpin()
 
 
 def make_params(max_depth, tmin, tmax, samples_per_pixel, image_width, image_height, sample_count=None,
@@ -390,11 +397,11 @@ def render(camera, world, max_depth, tmin, tmax, samples_per_pixel, image_width,
         return None
     p = make_params(max_depth, tmin, tmax, samples_per_pixel, image_width, image_height,
                     sample_count=sample_count, seed=seed, march_steps=march_steps, adaptive=adaptive)
-    if isinstance(pixels_box, PixelsBox) and p.width * p.height > 0:
-        pixels_box.pin()
     buf = pixels_box.pixels if isinstance(pixels_box, PixelsBox) else pixels_box
     if buf.dtype != L.PIXEL_STATS_DTYPE or buf.size != p.width * p.height or not buf.flags["C_CONTIGUOUS"]:
         raise ValueError("pixels must be a contiguous W*H om_pixel_stats array")
+    if isinstance(pixels_box, PixelsBox) and p.width * p.height > 0:
+        pixels_box.pin()
     ctr = L.om_counters()
     check(lib.om_render(world.ctx, C.byref(camera.raw), C.byref(p), buf.ctypes.data_as(C.c_void_p), C.byref(ctr)),
           world.ctx)

@@ -199,12 +199,14 @@ __device__ __forceinline__ F3 mbox_to_local(const OmMBox& B, F3 p) {
     return f3(p.x - B.center[0] * 1.0f, p.y - B.center[1] * 1.0f, p.z - B.center[2] * 1.0f);
 }
 __device__ __forceinline__ float mbox_sdf(const OmMBox& B, F3 p) { return mbox_local(B, mbox_to_local(B, p)); }
-// MarchedTorus (marched.rs:133-151)
-__device__ __forceinline__ float mtorus_local(const OmMTorus& T, F3 p) {
+// MarchedTorus (marched.rs:133-151); TT = OmMTorus or the march's SDF-only copy (om_trace.h)
+template <class TT>
+__device__ __forceinline__ float mtorus_local(const TT& T, F3 p) {
     const float qx = sqrtf((p.x * p.x + p.z * p.z) + 0.0f * 0.0f) - T.sizes[0];
     return sqrtf((qx * qx + p.y * p.y) + 0.0f * 0.0f) - T.sizes[1];
 }
-__device__ __forceinline__ F3 mtorus_to_local(const OmMTorus& T, F3 p) {
+template <class TT>
+__device__ __forceinline__ F3 mtorus_to_local(const TT& T, F3 p) {
     // Mat4x4::dot(p4 * w2l_s), p4 = (p, 1); only xyz are used by sdf
     const float s0 = p.x * T.w2l_s[0], s1 = p.y * T.w2l_s[1], s2 = p.z * T.w2l_s[2], s3 = 1.0f * T.w2l_s[3];
     const float* m = T.w2l_tr;
@@ -212,7 +214,8 @@ __device__ __forceinline__ F3 mtorus_to_local(const OmMTorus& T, F3 p) {
               m[4] * s0 + m[5] * s1 + m[6] * s2 + m[7] * s3,
               m[8] * s0 + m[9] * s1 + m[10] * s2 + m[11] * s3);
 }
-__device__ __forceinline__ float mtorus_sdf(const OmMTorus& T, F3 p) { return mtorus_local(T, mtorus_to_local(T, p)) * T.min_scale; }
+template <class TT>
+__device__ __forceinline__ float mtorus_sdf(const TT& T, F3 p) { return mtorus_local(T, mtorus_to_local(T, p)) * T.min_scale; }
 
 // get_outward_local_normal (marched.rs:25-44)
 template <class F>

@@ -38,12 +38,28 @@ __device__ __forceinline__ float inv_dir(float c) {
 
 // Work counters (om_counters); compiled out (COUNT=false) of the production kernels so
 // they cost no registers — the bench counts work in a separate, identical launch.
+// lap(k): the diagnostic build OM_PHASE_STAMPS=2 (tools/phase_stamps.py) splits the trace's
+// time into the steps below (every lap waits for outstanding memory first, so a lap after a
+// load measures that load's latency); a no-op otherwise.
+enum { LAP_ALWAYS2 = 0, LAP_NODE_WAIT, LAP_NODE_SLAB, LAP_POP, LAP_REC_WAIT, LAP_REC_TEST, LAP_N };
 template <bool COUNT>
 struct WorkT {
     uint32_t prim = 0, pre = 0, march = 0;
     __device__ __forceinline__ void add_prim() { if (COUNT) prim++; }
     __device__ __forceinline__ void add_pre(uint32_t k = 1) { if (COUNT) pre += k; }
     __device__ __forceinline__ void add_march() { if (COUNT) march++; }
+#if defined(OM_PHASE_STAMPS) && OM_PHASE_STAMPS == 2
+    uint64_t lt = 0, lacc[LAP_N] = {0, 0, 0, 0, 0, 0}, lcnt[LAP_N] = {0, 0, 0, 0, 0, 0};
+    __device__ __forceinline__ void lap_start() { __builtin_amdgcn_s_waitcnt(0); lt = __builtin_amdgcn_s_memtime(); }
+    __device__ __forceinline__ void lap(int k) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint64_t n = __builtin_amdgcn_s_memtime();
+        lacc[k] += n - lt; lcnt[k] += 1; lt = n;
+    }
+#else
+    __device__ __forceinline__ void lap_start() {}
+    __device__ __forceinline__ void lap(int) {}
+#endif
 };
 
 // Exact test of global primitive gi with the brute-force acceptance (root <= tmax).
@@ -157,6 +173,47 @@ __device__ __forceinline__ int traced_bvh(const OmSceneDev& S, F3 o, F3 d, float
     return best;
 }
 
+// A record at a wave-uniform address, read through the constant address space: scalar loads
+// (s_load, the scalar cache) instead of vector loads, which the compiler must otherwise use
+// because the kernels' global stores may alias the scene arrays (they never do: the scene is
+// immutable while a kernel runs, om_upload_world happens between calls).  The always2 records
+// are read by every ray of every wave: through the vector path each one was a dependent L2
+// round trip queued behind the path-state streams.
+#ifndef OM_A2_SCALAR
+#define OM_A2_SCALAR 1
+#endif
+template <class T>
+__device__ __forceinline__ T uniform_load(const T* p) {
+#if OM_A2_SCALAR
+    static_assert(sizeof(T) % 4 == 0, "dword records");
+    typedef const __attribute__((address_space(4))) uint32_t cu32;
+    cu32* q = (cu32*)p;
+    T r;
+    uint32_t* d = (uint32_t*)&r;
+#pragma unroll
+    for (uint32_t i = 0; i < sizeof(T) / 4; ++i) d[i] = q[i];
+    return r;
+#else
+    return *p;
+#endif
+}
+
+// Exact test of global primitive gi (wave-uniform) with the reference's acceptance, the record
+// read by uniform_load.
+template <class Wk>
+__device__ __forceinline__ void offer_uniform(const OmSceneDev& S, uint32_t gi, F3 o, F3 d, float tmin, float& closest, int& best,
+                                             Wk& w) {
+    float t, ndd;
+    bool h;
+    w.add_prim();
+    if (gi < S.off_cube) h = sphere_root(uniform_load(S.sph_test + gi), o, d, tmin, closest, t);
+    else if (gi < S.off_tri) { int ax; h = cube_root(uniform_load(S.cube_test + (gi - S.off_cube)), o, d, tmin, closest, t, ax); }
+    else if (gi < S.off_plane) h = bary_root<true>(uniform_load(S.tri + (gi - S.off_tri)), o, d, tmin, closest, t, ndd);
+    else if (gi < S.off_para) h = plane_root(uniform_load(S.plane + (gi - S.off_plane)), o, d, tmin, closest, t, ndd);
+    else h = bary_root<false>(uniform_load(S.para + (gi - S.off_para)), o, d, tmin, closest, t, ndd);
+    if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
+}
+
 // The primitives outside the BVH trees (always2): conservative box first, then the
 // exact test with the brute-force tie rule.  OM_DIAG_SPHERE: an unbounded record flagged as
 // an axis-aligned sphere takes sphere_root_diag (same accepted root, 24 fewer VALU).
@@ -167,7 +224,7 @@ template <class Wk>
 __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, float tmin, float ix, float iy, float iz,
                                               float nox, float noy, float noz, float t_lo, float& closest, int& best, Wk& w) {
     for (uint32_t k = 0; k < S.n_always2; ++k) {
-        const OmAlwaysRec A = S.always2_rec[k];
+        const OmAlwaysRec A = uniform_load(S.always2_rec + k);
 #ifndef OM_ALWAYS2_INF_SLAB
         // an unbounded record (huge primitives, planes: lo = -inf) passes every slab test
         if (A.lo[0] == -INFINITY) {
@@ -175,13 +232,13 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
             if (A.pad == OM_ALWAYS_DIAG_SPHERE && tmin > 0.0f) {                // axis-aligned sphere (the ground)
                 float t;
                 w.add_prim();
-                if (sphere_root_diag(S.sph_test[A.gi], o, d, tmin, closest, t) && (t < closest || (int)A.gi > best)) {
+                if (sphere_root_diag(uniform_load(S.sph_test + A.gi), o, d, tmin, closest, t) && (t < closest || (int)A.gi > best)) {
                     closest = t; best = (int)A.gi;
                 }
                 continue;
             }
 #endif
-            offer(S, A.gi, o, d, tmin, closest, best, w);
+            offer_uniform(S, A.gi, o, d, tmin, closest, best, w);
             continue;
         }
 #endif
@@ -192,7 +249,7 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
         const float z0 = __builtin_fmaf(A.lo[2], iz, noz), z1 = __builtin_fmaf(A.hi[2], iz, noz);
         const float n0 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
         const float f0 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
-        if (!(n0 > f0)) offer(S, A.gi, o, d, tmin, closest, best, w);
+        if (!(n0 > f0)) offer_uniform(S, A.gi, o, d, tmin, closest, best, w);
     }
 }
 
@@ -205,8 +262,10 @@ __device__ __forceinline__ void test_rec(const OmAffineTest& R, F3 o, F3 d, floa
     float t;
     int ax;
     w.add_prim();
+    w.lap(LAP_REC_WAIT);
     const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root(R, o, d, tmin, closest, t);
     if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
+    w.lap(LAP_REC_TEST);
 }
 
 // Leaf of the BVH2/BVH4: its records, tested in place.
@@ -267,14 +326,19 @@ __device__ __forceinline__ int traced_sbvh(const OmSceneDev& S, const OmSkipNode
     return best;
 }
 
-// The marched objects of a world, seen by the march loop through one of two views:
+// The marched objects of a world, seen by the march loop through one of three views:
 //  MarchedArrays  the scene arrays, any count (each step reloads every object's parameters
 //                 with scalar loads: runtime-bounded loops over memory);
 //  MarchedRegs    a copy of at most KS spheres, KB boxes and KT tori taken once before the
-//                 loop, so the parameters stay in (scalar) registers across the steps.
-// Both visit the objects in the same order with the same arithmetic.
+//                 loop, so the parameters stay in (scalar) registers across the steps;
+//  MarchedExact   a copy of EXACTLY NS spheres, NB boxes and NT tori with only the fields the
+//                 march reads (a torus: 24 of its 43 floats), taken once per kernel: fully
+//                 unrolled steps with no count guards, the parameters in SGPRs.
+// All visit the objects in the same order with the same arithmetic.  INDEXED: the view may be
+// indexed at run time (arrays); the register views are only ever indexed by unrolled counters.
 struct MarchedArrays {
     static constexpr uint32_t KS = 0u, KB = 0u, KT = 0u;      // 0: unbounded
+    static constexpr bool INDEXED = true;
     const OmMSphere* s; const OmMBox* b; const OmMTorus* t;
     uint32_t ns, nb, nt;
     __device__ explicit MarchedArrays(const OmSceneDev& S)
@@ -283,6 +347,7 @@ struct MarchedArrays {
 template <uint32_t KS_, uint32_t KB_, uint32_t KT_>
 struct MarchedRegs {
     static constexpr uint32_t KS = KS_, KB = KB_, KT = KT_;
+    static constexpr bool INDEXED = false;
     OmMSphere s[KS]; OmMBox b[KB]; OmMTorus t[KT];
     uint32_t ns, nb, nt;
     __device__ explicit MarchedRegs(const OmSceneDev& S) : ns(S.n_msph), nb(S.n_mbox), nt(S.n_mtor) {
@@ -297,7 +362,39 @@ struct MarchedRegs {
 };
 using MarchedSmall = MarchedRegs<4, 2, 1>;   // S-marched (2, 1, 1), S-full (0, 0, 1)
 
-// for (i < n) body(i): unrolled over the register view's bound, a plain loop otherwise
+// What mtorus_sdf and the march cull read of a torus (mtorus_to_local uses the first three
+// rows of W2L_TR and all of w2l_s, mtorus_local the two sizes): 24 floats of the 43.
+struct MTorusSdf {
+    float w2l_tr[12]; float w2l_s[4]; float sizes[2]; float min_scale, bk, br; float bc[3];
+    __device__ void load(const OmMTorus& T) {
+#pragma unroll
+        for (int k = 0; k < 12; ++k) w2l_tr[k] = T.w2l_tr[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w2l_s[k] = T.w2l_s[k];
+        sizes[0] = T.sizes[0]; sizes[1] = T.sizes[1];
+        min_scale = T.min_scale; bk = T.bk; br = T.br;
+        bc[0] = T.bc[0]; bc[1] = T.bc[1]; bc[2] = T.bc[2];
+    }
+};
+template <uint32_t NS, uint32_t NB, uint32_t NT>
+struct MarchedExact {
+    static constexpr uint32_t KS = NS, KB = NB, KT = NT;      // for_objects: unrolled (0: no loop)
+    static constexpr bool INDEXED = false;
+    static constexpr uint32_t ns = NS, nb = NB, nt = NT;
+    OmMSphere s[NS ? NS : 1]; OmMBox b[NB ? NB : 1]; MTorusSdf t[NT ? NT : 1];
+    __device__ explicit MarchedExact(const OmSceneDev& S) {
+#pragma unroll
+        for (uint32_t i = 0; i < NS; ++i) s[i] = S.msph[i];
+#pragma unroll
+        for (uint32_t i = 0; i < NB; ++i) b[i] = S.mbox[i];
+#pragma unroll
+        for (uint32_t i = 0; i < NT; ++i) t[i].load(S.mtor[i]);
+    }
+    __host__ __device__ static bool matches(uint32_t n_s, uint32_t n_b, uint32_t n_t) { return n_s == NS && n_b == NB && n_t == NT; }
+};
+
+// for (i < n) body(i): unrolled over the register view's bound, a plain loop otherwise (K = 0:
+// the arrays view's runtime count, or an exact view's constant 0, which folds away)
 template <uint32_t K, class F>
 __device__ __forceinline__ void for_objects(uint32_t n, F body) {
     if constexpr (K == 0u) {
@@ -392,7 +489,7 @@ __device__ __forceinline__ float nearest_marched_pf(const MarchedArrays& m, F3 p
 
 template <class M>
 __device__ __forceinline__ float nearest_marched(const M& m, F3 p, int& bk, uint32_t& bi) {
-    if constexpr (OM_MARCH_PREFETCH && M::KS == 0u) return nearest_marched_pf(m, p, bk, bi);
+    if constexpr (OM_MARCH_PREFETCH && M::INDEXED) return nearest_marched_pf(m, p, bk, bi);
     float best = INFINITY;
     bk = -1; bi = 0;
     for_objects<M::KS>(m.ns, [&](uint32_t i) {
@@ -408,7 +505,7 @@ __device__ __forceinline__ float nearest_marched(const M& m, F3 p, int& bk, uint
         if (v < best) { best = v; bk = 1; bi = i; }
     });
     for_objects<M::KT>(m.nt, [&](uint32_t i) {
-        const OmMTorus& T = m.t[i];
+        const auto& T = m.t[i];
         const float dx = p.x - T.bc[0], dy = p.y - T.bc[1], dz = p.z - T.bc[2];
         const float thr = best * T.bk + T.br;                                  // inf/NaN -> evaluate
         if (dx * dx + dy * dy + dz * dz > thr * thr) return;
@@ -422,7 +519,7 @@ __device__ __forceinline__ float nearest_marched(const M& m, F3 p, int& bk, uint
 // by unrolled loop counters (a runtime index would move it to scratch memory).
 template <class M>
 __device__ __forceinline__ float sdf_one(const M& m, int kind, uint32_t idx, F3 q) {
-    if constexpr (M::KS == 0u) {
+    if constexpr (M::INDEXED) {
         return kind == 0 ? fabsf(msphere_sdf(m.s[idx], q)) : kind == 1 ? fabsf(mbox_sdf(m.b[idx], q)) : fabsf(mtorus_sdf(m.t[idx], q));
     } else {
         float v = 0.0f;
@@ -489,7 +586,7 @@ __device__ __forceinline__ bool march_escapes(const M& m, F3 o, F3 d, F3 p, floa
         clear(B.center[0], B.center[1], B.center[2], (HIT + B.br) * 1.0001f);
     });
     for_objects<M::KT>(m.nt, [&](uint32_t i) {
-        const OmMTorus& Q = m.t[i];
+        const auto& Q = m.t[i];
         clear(Q.bc[0], Q.bc[1], Q.bc[2], HIT * Q.bk + Q.br);
     });
     return esc;
@@ -661,6 +758,9 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
 
 // HYB: only nodes [0, nl) are in `nodes` (the breadth-first prefix staged in LDS); the
 // others are read from `gnodes` (global memory, through L2).
+#ifndef OM_B2_TOS
+#define OM_B2_TOS 0
+#endif
 template <int DEPTH, int STRIDE, class Wk, bool HYB = false>
 __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node* nodes, const uint32_t* leaves,
                                            const OmAffineTest* recs, uint16_t* stk,
@@ -673,19 +773,40 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
     const float iz = inv_dir(d.z);
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
+    w.lap_start();
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
+    w.lap(LAP_ALWAYS2);
     uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
     int sp = 0;
     bool overflow = false;
+#if OM_B2_TOS
+    // the stack's top entry lives in a register: a pop takes it at once and re-reads the next
+    // one from LDS off the critical path (needed only at the next pop); LDS holds sp - 1 entries
+    uint32_t tos = 0;
+#define OM_B2_POP()                                                   \
+    do {                                                              \
+        cur = tos; --sp;                                              \
+        if (sp > 0) tos = stk[(sp - 1) * STRIDE];                     \
+    } while (0)
+#define OM_B2_PUSH(c)                                                 \
+    do {                                                              \
+        if (sp > 0) stk[(sp - 1) * STRIDE] = (uint16_t)tos;           \
+        tos = (c); ++sp;                                              \
+    } while (0)
+#else
+#define OM_B2_POP() do { --sp; cur = stk[sp * STRIDE]; } while (0)
+#define OM_B2_PUSH(c) do { stk[sp * STRIDE] = (uint16_t)(c); ++sp; } while (0)
+#endif
     for (;;) {
         if (cur & OM_LEAF) {                            // the single leaf site
             test_leaf(recs, leaves[cur & (OM_LEAF - 1u)], o, d, tmin, closest, best, w);
             if (sp == 0) break;
-            --sp;
-            cur = stk[sp * STRIDE];
+            OM_B2_POP();
+            w.lap(LAP_POP);
             continue;
         }
         const OmBvh2Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
+        w.lap(LAP_NODE_WAIT);
         w.add_pre(2);
         const float t_hi = closest * 1.0001f + 1e-3f;
 #if OM_PK_SLAB
@@ -717,17 +838,22 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
         if (h0 && h1) {                                 // near child next, far child pushed
             const bool swap = n1 < n0;
             const uint32_t nearc = swap ? N.c1 : N.c0, farc = swap ? N.c0 : N.c1;
-            if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)farc; ++sp; }
+            if (sp < DEPTH) OM_B2_PUSH(farc);
             else overflow = true;
             cur = nearc;
         } else if (h0 || h1) {
             cur = h0 ? N.c0 : N.c1;
         } else {
+            w.lap(LAP_NODE_SLAB);
             if (sp == 0) break;
-            --sp;
-            cur = stk[sp * STRIDE];
+            OM_B2_POP();
+            w.lap(LAP_POP);
+            continue;
         }
+        w.lap(LAP_NODE_SLAB);
     }
+#undef OM_B2_POP
+#undef OM_B2_PUSH
     (void)overflow;  // unreachable: om_upload_world enables BVH2 only when depth <= DEPTH
     return best;
 }

@@ -152,6 +152,16 @@ __host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
 #ifndef OM_WF_MARCH_REGS
 #define OM_WF_MARCH_REGS 0
 #endif
+// k_march instance for a marched set of exactly C2's shape (2 spheres, 1 box, 1 torus: S-marched):
+// MarchedExact, the SDF-only fields copied to SGPRs once per workgroup and every march step
+// unrolled with no count guards.  Traced parts TR_BRUTE / TR_BVH2_LDS only.
+#ifndef OM_WF_MARCH_EXACT
+#define OM_WF_MARCH_EXACT 1
+#endif
+using MarchedC2 = MarchedExact<2, 1, 1>;
+enum { MV_ARRAYS = 0, MV_SMALL = 1, MV_EXACT_C2 = 2 };
+template <int TR>
+__host__ __device__ constexpr bool exact_view_built() { return OM_WF_MARCH_EXACT && (TR == TR_BRUTE || TR == TR_BVH2_LDS); }
 // k_march refills its idle lanes once at least this many of a wave's 64 wait.
 #ifndef OM_WF_REFILL
 #define OM_WF_REFILL 16
@@ -189,6 +199,50 @@ __host__ __device__ inline uint32_t seg_capacity(uint64_t paths, uint32_t nseg) 
 }
 
 extern __shared__ __attribute__((aligned(16))) uint4 wf_lds[];
+
+// Diagnostic build only (OM_PHASE_STAMPS=1, tools/phase_stamps.py): every wave sums the shader
+// cycles (s_memtime) its lanes spend in each phase of a path chunk, and lane 0 adds the sums to
+// g_phase[kernel * 8 + phase] at exit.  Production builds compile none of it.
+#ifndef OM_PHASE_STAMPS
+#define OM_PHASE_STAMPS 0
+#endif
+#if OM_PHASE_STAMPS
+__device__ unsigned long long g_phase[64];
+enum { PHK_BOUNCE0 = 0, PHK_BOUNCE = 8, PHK_TAIL = 16, PHK_MARCH = 24, PHK_HIT = 32 };
+struct PhaseClock {
+    uint64_t t, begin, acc[6] = {0, 0, 0, 0, 0, 0};
+    __device__ PhaseClock() { t = begin = __builtin_amdgcn_s_memtime(); }
+    __device__ void lap(int k) { const uint64_t n = __builtin_amdgcn_s_memtime(); acc[k] += n - t; t = n; }
+    __device__ void flush(int base) {
+        const uint64_t life = __builtin_amdgcn_s_memtime() - begin;
+        if (__lane_id() == 0) {
+            for (int k = 0; k < 6; ++k) atomicAdd(&g_phase[base + k], (unsigned long long)acc[k]);
+            atomicAdd(&g_phase[base + 6], (unsigned long long)life);
+            atomicAdd(&g_phase[base + 7], 1ull);                    // waves
+        }
+    }
+};
+// OM_PHASE_STAMPS=2: the trace's laps (WorkT::lap, om_trace.h), summed over the lanes of every
+// wave (a lane's sums cover the steps it took part in) -> g_phase[40 + k] cycles, [48 + k] laps
+template <class Wk>
+__device__ void flush_laps(const Wk& w) {
+#if OM_PHASE_STAMPS == 2
+    for (int k = 0; k < LAP_N; ++k) {
+        atomicAdd(&g_phase[40 + k], (unsigned long long)w.lacc[k]);
+        atomicAdd(&g_phase[48 + k], (unsigned long long)w.lcnt[k]);
+    }
+#endif
+}
+#define PH_DECL PhaseClock ph_
+#define PH_LAP(k) ph_.lap(k)
+#define PH_WAIT_LAP(k) do { __builtin_amdgcn_s_waitcnt(0); ph_.lap(k); } while (0)
+#define PH_FLUSH(base) ph_.flush(base)
+#else
+#define PH_DECL
+#define PH_LAP(k)
+#define PH_WAIT_LAP(k)
+#define PH_FLUSH(base)
+#endif
 
 // Block-wide stream compaction: returns this lane's rank among the block's keep=true
 // lanes (lane order), and the block total.  Every thread of the block must call it.
@@ -437,6 +491,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
     WorkT<COUNT> w;
     uint32_t segs = 0, run = 0;
+    PH_DECL;
 #if OM_WF_WAVEQ
     const uint32_t lane = __lane_id();
     for (uint32_t chunk = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); chunk * 64u < n;) {   // wave-uniform
@@ -459,6 +514,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
                 load_rest(in, i, p);       // issued before the trace: its latency hides behind it
 #endif
             }
+            PH_WAIT_LAP(0);
             if (live) {
                 float closest;
                 int best;
@@ -490,6 +546,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
 #if !OM_WF_EARLY_REST
                 if (!FIRST) load_rest(in, i, p);
 #endif
+                PH_WAIT_LAP(1);
 #ifdef OM_ABLATE_SHADE2X   // timing ablation: shade a copy first (same result slot, same values)
                 {
                     Path p2 = p;
@@ -499,6 +556,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
 #endif
                 keep = shade_path<MARCH>(S, P, depth_cap, p, closest, best, res, res_id);
                 if (COUNT) segs++;
+                PH_WAIT_LAP(2);
             }
         }
 #if OM_WF_WAVEQ
@@ -511,7 +569,12 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
         obase = __builtin_amdgcn_readfirstlane(obase);
         chunk = __builtin_amdgcn_readfirstlane(nc);
         if (keep) store_path(out, seg0 + obase + (uint32_t)__popcll(m & ((1ull << lane) - 1ull)), p);
+        PH_WAIT_LAP(3);
     }
+    PH_FLUSH(HIT ? PHK_HIT : FIRST ? PHK_BOUNCE0 : PHK_BOUNCE);
+#if OM_PHASE_STAMPS
+    if (!FIRST && !HIT) flush_laps(w);
+#endif
     __syncthreads();
     run = q_out;
 #else
@@ -575,6 +638,7 @@ __device__ __forceinline__ void march_lanes(const OmSceneDev& S, const OmParamsD
     float t = 0.0f, closest = 0.0f;
     int best = -1;
     uint32_t iters = 0;
+    PH_DECL;
     auto start = [&]() {
         const float4 a = in.q0[seg0 + j], b = in.q1[seg0 + j];
         o = f3(a.x, a.y, a.z); d = f3(b.x, b.y, b.z);
@@ -583,6 +647,7 @@ __device__ __forceinline__ void march_lanes(const OmSceneDev& S, const OmParamsD
         iters = P.march_steps;
     };
     if (act) start();
+    PH_WAIT_LAP(0);
     for (;;) {
         if (act) {
             int gi = -1;
@@ -593,6 +658,7 @@ __device__ __forceinline__ void march_lanes(const OmSceneDev& S, const OmParamsD
                 act = false;
             }
         }
+        PH_WAIT_LAP(1);
         // refill the idle lanes together once enough of them wait (or nothing else runs):
         // a refill runs the trace and unstuck, which costs several march steps
         const uint64_t want = __ballot(!act && !dry), busy = __ballot(act);
@@ -604,12 +670,15 @@ __device__ __forceinline__ void march_lanes(const OmSceneDev& S, const OmParamsD
                 j = base + (uint32_t)__popcll(want & ((1ull << lane) - 1ull));
                 if (j < n) { act = true; start(); } else dry = true;
             }
+            PH_WAIT_LAP(0);
         }
+        PH_LAP(3);
         if (__ballot(act) == 0) break;
     }
+    PH_FLUSH(PHK_MARCH);
 }
 
-template <int TR, bool COUNT, bool SMALL>
+template <int TR, bool COUNT, int VIEW>
 __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_march(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
                                                 const uint32_t* __restrict__ count_in, float2* __restrict__ hit,
                                                 unsigned long long* __restrict__ counters) {
@@ -621,7 +690,8 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_march(OmSceneDev S, OmPa
     __syncthreads();
     const Tracer T = stage_scene<TR>(S);
     WorkT<COUNT> w;
-    if constexpr (SMALL) march_lanes<TR, COUNT>(S, P, T, MarchedSmall(S), in, seg0, n, next, hit, w);
+    if constexpr (VIEW == MV_EXACT_C2) march_lanes<TR, COUNT>(S, P, T, MarchedC2(S), in, seg0, n, next, hit, w);
+    else if constexpr (VIEW == MV_SMALL) march_lanes<TR, COUNT>(S, P, T, MarchedSmall(S), in, seg0, n, next, hit, w);
     else march_lanes<TR, COUNT>(S, P, T, MarchedArrays(S), in, seg0, n, next, hit, w);
     if (COUNT) {
         flush_counter(counters, OMC_PRIM_TESTS, w.prim);
@@ -656,6 +726,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmPar
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
     WorkT<COUNT> w;
     uint32_t segs = 0;
+    PH_DECL;
     for (uint32_t idx = threadIdx.x; idx < total; idx = atomicAdd(&next, 1u)) {
         uint32_t k = 0;
         while (idx >= pre[k + 1]) ++k;
@@ -663,13 +734,18 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmPar
         Path p;
         load_ray(in, i, p);
         load_rest(in, i, p);
+        PH_WAIT_LAP(0);
         for (;;) {
             float closest;
             const int best = trace<TR, MARCH>(S, P, T, p.o, p.d, closest, w);
             if (COUNT) segs++;
-            if (!shade_path<MARCH>(S, P, depth_cap, p, closest, best, res, res_id)) break;
+            PH_WAIT_LAP(1);
+            const bool more = shade_path<MARCH>(S, P, depth_cap, p, closest, best, res, res_id);
+            PH_WAIT_LAP(2);
+            if (!more) break;
         }
     }
+    PH_FLUSH(PHK_TAIL);
     if (COUNT) {
         flush_counter(counters, OMC_SEGMENTS, segs);
         flush_counter(counters, OMC_PRIM_TESTS, w.prim);
@@ -814,10 +890,19 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
             int ti = each ? tm.begin(st) : -1;
             const bool small = OM_WF_MARCH_REGS && L.S.n_msph <= MarchedSmall::KS && L.S.n_mbox <= MarchedSmall::KB &&
                                L.S.n_mtor <= MarchedSmall::KT;
+            const bool exact = MarchedC2::matches(L.S.n_msph, L.S.n_mbox, L.S.n_mtor);
+            if constexpr (exact_view_built<TR>()) {
+                if (exact) {
+                    hipLaunchKernelGGL((k_march<TR, COUNT, MV_EXACT_C2>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin,
+                                       B.hit, L.counters);
+                    goto launched;
+                }
+            }
             if (small)
-                hipLaunchKernelGGL((k_march<TR, COUNT, true>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin, B.hit, L.counters);
+                hipLaunchKernelGGL((k_march<TR, COUNT, MV_SMALL>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin, B.hit, L.counters);
             else
-                hipLaunchKernelGGL((k_march<TR, COUNT, false>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin, B.hit, L.counters);
+                hipLaunchKernelGGL((k_march<TR, COUNT, MV_ARRAYS>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin, B.hit, L.counters);
+        launched:
             tm.end(ti, kc, st);
             ti = each ? tm.begin(st) : -1;
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false, true>), dim3(G.nseg), dim3(kBlk), 0, st, L.S, L.P, G, R, in,
@@ -1038,3 +1123,15 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
 }
 
 }  // namespace omw
+
+#if OM_PHASE_STAMPS
+// diagnostic build only: copy (and optionally clear) the phase sums
+extern "C" int om_debug_phase_stamps(unsigned long long* out64, int reset) {
+    if (hipMemcpyFromSymbol(out64, HIP_SYMBOL(omw::g_phase), sizeof(omw::g_phase)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long zero[64] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(omw::g_phase), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif

@@ -102,16 +102,3 @@ def test_c0_frame_bit_exact(om, oracle, pipeline):
     assert nb == 0, msg
     assert (got["n"] == SPP).all()
 
-
-@pytest.mark.parametrize("pipeline", PIPELINES)
-def test_nan_marched_normal_payload_bits(om, oracle, pipeline):
-    """The strict form of test_nan_marched_normal: the NaN payloads too, byte for byte.  The
-    NaNs here come from 0 * inf in unit((0, 0, 0)) and then only propagate (gfx950 and x86 both
-    give 0x7FC00000 for it), so the frames are expected to match exactly."""
-    W, H, SPP = 64, 40, 4
-    w, ow = nan_normal_world(om, oracle)
-    cam, ocam = om.default_camera(W / H), oracle.default_camera(W / H)
-    exp, _ = oracle.render(ow, ocam, oracle.params(W, H, SPP, seed=31, march_steps=256))
-    got = _render(om, w, cam, W, H, SPP, "auto", pipeline, seed=31, march_steps=256)
-    nb, msg = compare_stats(got, exp, f"nan-normal bits/{pipeline}")
-    assert nb == 0, msg

@@ -94,6 +94,15 @@ declare -A V=(
   [memclause]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-memory-clause"
   [bias0]="$COMMON $DEV -mllvm -amdgpu-schedule-metric-bias=0"
   [tprio0]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0"
+  # r03: C2's k_march with the SDF-only exact register view (default on) or the arrays view
+  [noexact]="$COMMON $DEV -DOM_WF_MARCH_EXACT=0"
+  # r03: diagnostic build, per-phase wave cycles (tools/phase_stamps.py)
+  [phase]="$COMMON $DEV -DOM_PHASE_STAMPS=1"
+  [phase2]="$COMMON $DEV -DOM_PHASE_STAMPS=2"
+  # r03: BVH2 stack top in a register (the pop's LDS read off the critical path)
+  [tos]="$COMMON $DEV -DOM_B2_TOS=1"
+  # r03: always2 records through scalar loads (default on) or vector loads
+  [a2vec]="$COMMON $DEV -DOM_A2_SCALAR=0"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
