@@ -859,6 +859,114 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
 }
 
 
+// Two rays per lane through the LDS BVH2 (OM_WF_DUAL): each iteration issues
+// one 64-B fetch per live ray -- its next node from LDS, or its next leaf record from global
+// memory -- for BOTH rays before either is consumed, then advances each ray by that one step.
+// A lane thus keeps two independent dependent chains in flight (one ray's node or record read
+// overlaps the other's slab or quadratic).  Per ray the visit order, the tests and the
+// acceptance rule are those of traced_bvh2 (near child first, brute-force tie rule), so the
+// winner is bit-identical.  Leaves are walked one record per iteration.
+struct B2Ray {
+    F3 o, d;
+    float ix, iy, iz;
+    float closest;
+    int best;
+    uint32_t cur;          // node to visit when no leaf record is pending
+    uint32_t leaf;         // (next leaf record << 8) | records left; 0: visit node cur
+    int sp;                // lane-stack depth; < 0: the ray is done
+    __device__ __forceinline__ bool live() const { return sp >= 0; }
+};
+
+// Continue at child code c: a node, or a leaf (its records; an empty leaf pops on).
+template <int STRIDE>
+__device__ __forceinline__ void b2_enter(B2Ray& r, uint32_t c, const uint32_t* leaves, const uint16_t* stk) {
+    for (;;) {
+        if (!(c & OM_LEAF)) { r.cur = c; return; }
+        const uint32_t lf = leaves[c & (OM_LEAF - 1u)];
+        if (lf & 255u) { r.leaf = lf; return; }
+        if (--r.sp < 0) return;
+        c = stk[r.sp * STRIDE];
+    }
+}
+template <int STRIDE>
+__device__ __forceinline__ void b2_pop(B2Ray& r, const uint32_t* leaves, const uint16_t* stk) {
+    if (--r.sp < 0) return;
+    b2_enter<STRIDE>(r, stk[r.sp * STRIDE], leaves, stk);
+}
+
+// Ray setup: the non-finite answer, or always2 and the root.
+template <class Wk>
+__device__ __forceinline__ void b2_begin(const OmSceneDev& S, B2Ray& r, F3 o, F3 d, float tmin, float tmax, Wk& w) {
+    r.o = o; r.d = d; r.closest = tmax; r.best = -1; r.cur = 0; r.leaf = 0; r.sp = 0;
+    r.ix = r.iy = r.iz = 0.0f;
+    if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) { r.best = nonfinite_hit(S, r.closest); r.sp = -1; return; }
+    r.ix = inv_dir(d.x); r.iy = inv_dir(d.y); r.iz = inv_dir(d.z);
+    offer_always2(S, o, d, tmin, r.ix, r.iy, r.iz, -o.x * r.ix, -o.y * r.iy, -o.z * r.iz, tmin * 0.5f - 1e-3f, r.closest,
+                  r.best, w);
+}
+
+// The 64 B a live ray needs next: a leaf record (global) or a node (LDS).
+__device__ __forceinline__ void b2_fetch(const B2Ray& r, const OmBvh2Node* nodes, const OmAffineTest* recs, uint4 (&q)[4]) {
+    if (!r.live()) return;
+    const uint4* src = r.leaf ? (const uint4*)(recs + (r.leaf >> 8)) : (const uint4*)(nodes + r.cur);
+    q[0] = src[0]; q[1] = src[1]; q[2] = src[2]; q[3] = src[3];
+}
+
+// One step of a live ray with its fetched 64 B.
+template <int DEPTH, int STRIDE, class Wk>
+__device__ __forceinline__ void b2_step(B2Ray& r, const uint4 (&q)[4], const uint32_t* leaves, uint16_t* stk, float tmin,
+                                        Wk& w) {
+    if (!r.live()) return;
+    if (r.leaf) {                                                   // one leaf record
+        OmAffineTest R;
+        __builtin_memcpy(&R, q, sizeof(R));
+        test_rec(R, r.o, r.d, tmin, r.closest, r.best, w);
+        r.leaf += 255u;                                             // next record, one fewer left
+        if (!(r.leaf & 255u)) { r.leaf = 0; b2_pop<STRIDE>(r, leaves, stk); }
+        return;
+    }
+    OmBvh2Node N;                                                   // one node: both child boxes
+    __builtin_memcpy(&N, q, sizeof(N));
+    w.add_pre(2);
+    const float nox = -r.o.x * r.ix, noy = -r.o.y * r.iy, noz = -r.o.z * r.iz;
+    const float t_lo = tmin * 0.5f - 1e-3f, t_hi = r.closest * 1.0001f + 1e-3f;
+    float x0 = __builtin_fmaf(N.lo0[0], r.ix, nox), x1 = __builtin_fmaf(N.hi0[0], r.ix, nox);
+    float y0 = __builtin_fmaf(N.lo0[1], r.iy, noy), y1 = __builtin_fmaf(N.hi0[1], r.iy, noy);
+    float z0 = __builtin_fmaf(N.lo0[2], r.iz, noz), z1 = __builtin_fmaf(N.hi0[2], r.iz, noz);
+    const float n0 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
+    const float f0 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
+    x0 = __builtin_fmaf(N.lo1[0], r.ix, nox); x1 = __builtin_fmaf(N.hi1[0], r.ix, nox);
+    y0 = __builtin_fmaf(N.lo1[1], r.iy, noy); y1 = __builtin_fmaf(N.hi1[1], r.iy, noy);
+    z0 = __builtin_fmaf(N.lo1[2], r.iz, noz); z1 = __builtin_fmaf(N.hi1[2], r.iz, noz);
+    const float n1 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
+    const float f1 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
+    const bool h0 = !(n0 > f0), h1 = !(n1 > f1);
+    if (h0 && h1) {
+        const bool swap = n1 < n0;
+        const uint32_t nearc = swap ? N.c1 : N.c0, farc = swap ? N.c0 : N.c1;
+        if (r.sp < DEPTH) { stk[r.sp * STRIDE] = (uint16_t)farc; ++r.sp; }
+        b2_enter<STRIDE>(r, nearc, leaves, stk);
+    } else if (h0 || h1) {
+        b2_enter<STRIDE>(r, h0 ? N.c0 : N.c1, leaves, stk);
+    } else {
+        b2_pop<STRIDE>(r, leaves, stk);
+    }
+}
+
+// Both rays to completion: -> closest / best of each, as traced_bvh2 would return them.
+template <int DEPTH, int STRIDE, class Wk>
+__device__ __forceinline__ void traced_bvh2_x2(const OmSceneDev& S, const OmBvh2Node* nodes, const uint32_t* leaves,
+                                               const OmAffineTest* recs, uint16_t* stkA, uint16_t* stkB, float tmin,
+                                               B2Ray& A, B2Ray& B, Wk& w) {
+    while (A.live() || B.live()) {
+        uint4 qa[4], qb[4];
+        b2_fetch(A, nodes, recs, qa);
+        b2_fetch(B, nodes, recs, qb);
+        b2_step<DEPTH, STRIDE>(A, qa, leaves, stkA, tmin, w);
+        b2_step<DEPTH, STRIDE>(B, qb, leaves, stkB, tmin, w);
+    }
+}
+
 // 4-wide BVH traversal: one 112-B node read gives four slab tests; the
 // hit children are ordered near-first by a 5-compare sorting network, the nearest is
 // visited next and the others go on the lane's LDS stack with three unconditional u16

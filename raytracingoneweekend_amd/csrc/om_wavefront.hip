@@ -336,7 +336,7 @@ struct Tracer {
     uint16_t* stk;
 };
 
-template <int TR>
+template <int TR, uint32_t STACKS = 1>
 __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every thread of the block calls it
     Tracer t;
     t.stk = (uint16_t*)wf_lds + threadIdx.x;
@@ -344,7 +344,7 @@ __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every 
     t.nl = 0; t.b2l = S.b2nodes;
     if (TR == TR_BVH2_GLOBAL && hyb_nodes(S)) {
         t.nl = hyb_nodes(S);
-        uint4* dst = wf_lds + stack_bytes<TR>(S) / 16u;
+        uint4* dst = wf_lds + STACKS * stack_bytes<TR>(S) / 16u;
         const uint4* sn = (const uint4*)S.b2nodes;
         for (uint32_t i = threadIdx.x; i < t.nl * 4u; i += kBlk) dst[i] = sn[i];
         __syncthreads();
@@ -353,7 +353,7 @@ __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every 
     if (TR == TR_BVH2_LDS || TR == TR_BVH4_LDS) {
         const uint32_t nn = TR == TR_BVH2_LDS ? S.n_b2nodes * 4u : S.n_b4nodes * 7u;   // uint4 per node
         const uint4* sn = TR == TR_BVH2_LDS ? (const uint4*)S.b2nodes : (const uint4*)S.b4nodes;
-        uint4* dst = wf_lds + stack_bytes<TR>(S) / 16u;
+        uint4* dst = wf_lds + STACKS * stack_bytes<TR>(S) / 16u;
         for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = sn[i];
         uint32_t* ldst = (uint32_t*)(dst + nn);
         for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += kBlk) ldst[i] = S.b2leaves[i];
@@ -585,6 +585,90 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
     }
 #endif
     if (threadIdx.x == 0) count_out[blockIdx.x] = run;
+    if (COUNT) {
+        flush_counter(counters, OMC_SEGMENTS, segs);
+        flush_counter(counters, OMC_PRIM_TESTS, w.prim);
+        flush_counter(counters, OMC_PRE_TESTS, w.pre);
+        flush_counter(counters, OMC_MARCH, w.march);
+    }
+}
+
+// ---------------------------------------------------------------- two paths per lane
+// OM_WF_DUAL: bounces b >= 1 of traced worlds whose BVH2 sits in LDS run
+// k_bounce2 instead of k_bounce: a wave takes 128-path chunks, lane l holds paths l and l + 64
+// of its chunk and traces both at once (traced_bvh2_x2: each iteration fetches the next node or
+// leaf record of BOTH rays before advancing either), then shades both and appends the survivors
+// of both with one LDS atomic.  The lane stack is doubled (second half: the B rays).  Results
+// are keyed by slot and (pixel, sample) as everywhere, so the bits are unchanged.
+#ifndef OM_WF_DUAL
+#define OM_WF_DUAL 0
+#endif
+#ifndef OM_WF_DUAL_WAVES
+#define OM_WF_DUAL_WAVES 0
+#endif
+#if OM_WF_DUAL_WAVES > 0
+#define OM_WAVES_ATTR_DUAL __attribute__((amdgpu_waves_per_eu(OM_WF_DUAL_WAVES, OM_WF_DUAL_WAVES)))
+#else
+#define OM_WAVES_ATTR_DUAL
+#endif
+template <bool COUNT>
+__global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_DUAL void k_bounce2(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
+                                                           const uint32_t* __restrict__ count_in, Queue out,
+                                                           uint32_t* __restrict__ count_out, float4* __restrict__ res,
+                                                           uint32_t* __restrict__ res_id,
+                                                           unsigned long long* __restrict__ counters) {
+    const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
+    const uint32_t n = count_in[blockIdx.x];
+    if (n == 0) {
+        if (threadIdx.x == 0) count_out[blockIdx.x] = 0u;
+        return;
+    }
+    __shared__ uint32_t q_next, q_out;
+    if (threadIdx.x == 0) { q_next = kBlk / 64u; q_out = 0u; }
+    __syncthreads();
+    const Tracer T = stage_scene<TR_BVH2_LDS, 2>(S);
+    uint16_t* stkB = T.stk + S.b2_stack * kBlk;
+    const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
+    WorkT<COUNT> w;
+    uint32_t segs = 0;
+    const uint32_t lane = __lane_id();
+    for (uint32_t chunk = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); chunk * 128u < n;) {   // wave-uniform
+        const uint32_t ja = chunk * 128u + lane, jb = ja + 64u;
+        const bool ina = ja < n, inb = jb < n;
+        Path pa, pb;
+        B2Ray A, B;
+        A.sp = -1; B.sp = -1;
+        if (ina) load_ray(in, seg0 + ja, pa);
+        if (inb) load_ray(in, seg0 + jb, pb);
+        if (ina) b2_begin(S, A, pa.o, pa.d, P.tmin, P.tmax, w);
+        if (inb) b2_begin(S, B, pb.o, pb.d, P.tmin, P.tmax, w);
+        traced_bvh2_x2<kStackDepth, kBlk>(S, T.b2n, T.bl, T.recs, T.stk, stkB, P.tmin, A, B, w);
+        bool ka = false, kb = false;
+        if (ina) {
+            load_rest(in, seg0 + ja, pa);
+            ka = shade_path<false>(S, P, depth_cap, pa, A.closest, A.best, res, res_id);
+            if (COUNT) segs++;
+        }
+        if (inb) {
+            load_rest(in, seg0 + jb, pb);
+            kb = shade_path<false>(S, P, depth_cap, pb, B.closest, B.best, res, res_id);
+            if (COUNT) segs++;
+        }
+        const uint64_t ma = __ballot(ka), mb = __ballot(kb);
+        uint32_t obase = 0u, nc = 0u;
+        if (lane == 0) {
+            const uint32_t c = (uint32_t)(__popcll(ma) + __popcll(mb));
+            obase = c ? atomicAdd(&q_out, c) : 0u;
+            nc = atomicAdd(&q_next, 1u);
+        }
+        obase = __builtin_amdgcn_readfirstlane(obase);
+        chunk = __builtin_amdgcn_readfirstlane(nc);
+        const uint64_t below = (1ull << lane) - 1ull;
+        if (ka) store_path(out, seg0 + obase + (uint32_t)__popcll(ma & below), pa);
+        if (kb) store_path(out, seg0 + obase + (uint32_t)__popcll(ma) + (uint32_t)__popcll(mb & below), pb);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) count_out[blockIdx.x] = q_out;
     if (COUNT) {
         flush_counter(counters, OMC_SEGMENTS, segs);
         flush_counter(counters, OMC_PRIM_TESTS, w.prim);
@@ -925,6 +1009,9 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         if (bounce == 0)
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, true>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
                                cin, out, cout, B.res, B.res_id, L.counters, (const float2*)nullptr);
+        else if (OM_WF_DUAL && TR == TR_BVH2_LDS && !MARCH)
+            hipLaunchKernelGGL((k_bounce2<COUNT>), dim3(G.nseg), dim3(kBlk), lds + stack_bytes<TR_BVH2_LDS>(L.S), st, L.S,
+                               L.P, G, in, cin, out, cout, B.res, B.res_id, L.counters);
         else
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
                                cin, out, cout, B.res, B.res_id, L.counters, (const float2*)nullptr);

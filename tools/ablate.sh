@@ -103,6 +103,10 @@ declare -A V=(
   [tos]="$COMMON $DEV -DOM_B2_TOS=1"
   # r03: always2 records through scalar loads (default on) or vector loads
   [a2vec]="$COMMON $DEV -DOM_A2_SCALAR=0"
+  # r03: two paths per lane in the later bounces (k_bounce2), occupancy request 0 (none) / 6 / 5
+  [dual]="$COMMON $DEV -DOM_WF_DUAL=1"
+  [dual6]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=6"
+  [dual5]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=5"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
