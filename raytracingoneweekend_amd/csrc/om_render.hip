@@ -420,7 +420,8 @@ om_status ensure_tile_lists(om_ctx* c, const om_camera* cam, uint32_t W, uint32_
         c->tiles_use = false;
         if (ok) {
             om_status s = ensure(c, c->tile_off, tl.off.size() * 4u);
-            if (s == OM_OK) s = ensure(c, c->tile_idx, std::max<size_t>(tl.idx.size(), 1u) * 2u);
+            // +1 entry: the uniform (scalar) reader loads whole dwords (traced_tiles<true>, om_trace.h)
+            if (s == OM_OK) s = ensure(c, c->tile_idx, (tl.idx.size() + 2u) * 2u);
             if (s != OM_OK) return s;
             OM_HIP(c, hipStreamSynchronize(stream));        // the previous lists may still be read
             OM_HIP(c, hipMemcpy(c->tile_off.p, tl.off.data(), tl.off.size() * 4u, hipMemcpyHostToDevice));

@@ -741,7 +741,10 @@ __device__ __forceinline__ int nonfinite_hit(const OmSceneDev& S, float& closest
 // Primary ray with a per-tile candidate list (om_tiles.h): always2, then
 // every record the conservative lens-aware frustum of its 8x8 tile can reach — the
 // brute-force loop of hits.rs:274-285 over a superset of the records it could accept.
-template <class Wk>
+// UNIFORM: every lane of the wave is in tile `tile` (the caller checked it; a bounce-0 wave is one
+// 8x8 tile of one sample except where partial tiles meet), so the list and its records are read
+// with scalar loads (uniform_load) instead of vector loads.
+template <bool UNIFORM = false, class Wk>
 __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t* toff, const uint16_t* tidx, uint32_t tile,
                                             F3 o, F3 d, float tmin, float& closest, Wk& w) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
@@ -751,8 +754,17 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
     const float iz = inv_dir(d.z);
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, tmin * 0.5f - 1e-3f, closest, best, w);
-    const uint32_t e = toff[tile + 1];
-    for (uint32_t k = toff[tile]; k < e; ++k) test_rec(S.srecs[tidx[k]], o, d, tmin, closest, best, w);
+    if constexpr (UNIFORM) {
+        const uint32_t b = uniform_load(toff + tile), e = uniform_load(toff + tile + 1);
+        const uint32_t* tw = (const uint32_t*)tidx;                 // u16 entries, read as the dword holding them
+        for (uint32_t k = b; k < e; ++k) {
+            const uint32_t pair = uniform_load(tw + (k >> 1));
+            test_rec(uniform_load(S.srecs + ((k & 1u) ? pair >> 16 : pair & 0xFFFFu)), o, d, tmin, closest, best, w);
+        }
+    } else {
+        const uint32_t e = toff[tile + 1];
+        for (uint32_t k = toff[tile]; k < e; ++k) test_rec(S.srecs[tidx[k]], o, d, tmin, closest, best, w);
+    }
     return best;
 }
 

@@ -126,6 +126,11 @@ constexpr uint32_t kTailDefault = 16;                             // first bounc
 #ifndef OM_WF_WAVEQ
 #define OM_WF_WAVEQ 1
 #endif
+// Bounce 0 with primary tile lists: a wave whose lanes all lie in one 8x8 tile (every wave but
+// those where partial tiles meet) reads the tile's list and records with scalar loads.
+#ifndef OM_TILES_UNIFORM
+#define OM_TILES_UNIFORM 1
+#endif
 // Segment capacity rounded up to whole waves (0: exact split), so that a bounce-0 wave is
 // exactly one 8x8 tile of one sample (tile-ordered pixel lists hold whole tiles).
 // A BVH2 too big for LDS (S-10k: 213 KB) stages its breadth-first prefix, up to this many
@@ -525,7 +530,14 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
                     const uint32_t line = p_pixel / P.width;
                     const uint32_t tile = (p_pixel - line * P.width) / 8u + (line / 8u) * P.tiles_x;
                     closest = P.tmax;
-                    best = traced_tiles(S, R.tile_off, R.tile_idx, tile, p.o, p.d, P.tmin, closest, w);
+#if OM_TILES_UNIFORM
+                    // a wave within one tile reads its list with scalar loads
+                    const uint32_t t0 = __builtin_amdgcn_readfirstlane(tile);
+                    if (__ballot(tile != t0) == 0)
+                        best = traced_tiles<true>(S, R.tile_off, R.tile_idx, t0, p.o, p.d, P.tmin, closest, w);
+                    else
+#endif
+                        best = traced_tiles(S, R.tile_off, R.tile_idx, tile, p.o, p.d, P.tmin, closest, w);
                     if (MARCH) {
                         float tm;
                         const int mg = march(S, p.o, p.d, P.tmin, P.tmax, closest, P.march_steps, tm, w);
@@ -1009,9 +1021,11 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         if (bounce == 0)
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, true>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
                                cin, out, cout, B.res, B.res_id, L.counters, (const float2*)nullptr);
-        else if (OM_WF_DUAL && TR == TR_BVH2_LDS && !MARCH)
+#if OM_WF_DUAL
+        else if (TR == TR_BVH2_LDS && !MARCH)
             hipLaunchKernelGGL((k_bounce2<COUNT>), dim3(G.nseg), dim3(kBlk), lds + stack_bytes<TR_BVH2_LDS>(L.S), st, L.S,
                                L.P, G, in, cin, out, cout, B.res, B.res_id, L.counters);
+#endif
         else
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
                                cin, out, cout, B.res, B.res_id, L.counters, (const float2*)nullptr);

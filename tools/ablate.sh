@@ -105,6 +105,8 @@ declare -A V=(
   [a2vec]="$COMMON $DEV -DOM_A2_SCALAR=0"
   # r03: two paths per lane in the later bounces (k_bounce2), occupancy request 0 (none) / 6 / 5
   [dual]="$COMMON $DEV -DOM_WF_DUAL=1"
+  # r03: bounce 0's tile lists through vector loads only (default: scalar when the wave is one tile)
+  [tilesvec]="$COMMON $DEV -DOM_TILES_UNIFORM=0"
   [dual6]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=6"
   [dual5]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=5"
 )
