@@ -263,14 +263,21 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     // compressed BVH2: both child boxes in the parent (one 64-B read per visit), emitted
     // breadth-first so the top levels, which every ray visits, are the first nodes: a tree
     // too big for LDS stages that prefix there (om_wavefront.hip, OM_WF_HYB_BYTES).
+    // direct leaf codes (OM_B2_DIRECT): when every record index fits 11 bits and every leaf holds
+    // at most 15 records (S-traced: 485 records, leaves <= 8), a leaf child's 16-bit code is
+    // OM_LEAF | first << 4 | count, so the traversal needs no leaf-table read to enter a leaf;
+    // the table is still emitted (same order) for the other consumers.
+    const bool direct = OM_B2_DIRECT && fw.srecs.size() < 2048u;
     struct Emit2 {
         const Builder& b; const std::vector<uint32_t>& leaf_first; std::vector<OmBvh2Node>& out;
         std::vector<uint32_t>& leaves;
+        bool direct;
         std::vector<std::pair<uint32_t, uint32_t>> q;   // (builder node, output index)
         uint32_t code(uint32_t c) {
             const OmBvhNode& n = b.nodes[c];
             if (n.left < 0) {
                 leaves.push_back((leaf_first[c] << 8) | (uint32_t)n.right);
+                if (direct) return OM_LEAF | (leaf_first[c] << 4) | (uint32_t)n.right;
                 return OM_LEAF | (uint32_t)(leaves.size() - 1);
             }
             out.push_back(OmBvh2Node{});
@@ -295,7 +302,7 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
                 out[idx] = o;
             }
         }
-    } e2{b, leaf_first, fw.b2nodes, fw.b2leaves, {}};
+    } e2{b, leaf_first, fw.b2nodes, fw.b2leaves, direct, {}};
     fw.b2nodes.clear();
     fw.b2leaves.clear();
     if (b.nodes[root].left < 0) {            // a single leaf: one node, second child an empty leaf
@@ -306,12 +313,13 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
         }
         fw.b2leaves.push_back((leaf_first[root] << 8) | (uint32_t)b.nodes[root].right);
         fw.b2leaves.push_back(0u);
-        o.c0 = OM_LEAF | 0u;
-        o.c1 = OM_LEAF | 1u;
+        o.c0 = direct ? (OM_LEAF | (leaf_first[root] << 4) | (uint32_t)b.nodes[root].right) : (OM_LEAF | 0u);
+        o.c1 = direct ? OM_LEAF : (OM_LEAF | 1u);          // empty leaf: no records
         fw.b2nodes.push_back(o);
     } else {
         e2.rec(root);
     }
+    fw.b2_direct = direct ? 1u : 0u;
     // depth of the compressed tree (the traversal's stack bound)
     std::vector<uint32_t> depth(fw.b2nodes.size(), 1);
     fw.b2_depth = 1;

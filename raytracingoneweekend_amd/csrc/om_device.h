@@ -267,7 +267,27 @@ __device__ __forceinline__ float reflectance(float c, float ref_idx) {          
 }
 // Material::scatter (materials.rs:39-95); returns the unnormalised new direction
 // (Ray::new normalises it, ray.rs:11-13) and the attenuation.
+// OM_SCATTER_SHARED_SPHERE (default 1): Lambertian and Metal both draw one rand_in_unit_sphere
+// before anything else that consumes the stream (reflect draws nothing), so a wave holding both
+// kinds runs ONE rejection loop for them instead of one per kind; each path's draws are unchanged.
+#ifndef OM_SCATTER_SHARED_SPHERE
+#define OM_SCATTER_SHARED_SPHERE 1
+#endif
 __device__ __forceinline__ void scatter(const OmMaterial& m, F3 dir, F3 normal, Rng& g, F3& new_dir, F3& atten) {
+#if OM_SCATTER_SHARED_SPHERE
+    if (m.type != 2) {
+        const F3 r = rand_in_unit_sphere(g);                                                     // materials.rs:54 / :64
+        if (m.type == 0) {                                                                       // lambertian :52-61
+            F3 nd = add(normal, unit(r));
+            if (fabsf(nd.x) < 1e-8f && fabsf(nd.y) < 1e-8f && fabsf(nd.z) < 1e-8f) nd = normal;  // near_zero vec3.rs:69-72
+            new_dir = nd;
+        } else {                                                                                 // metal :62-66
+            const F3 refl = reflect(dir, normal);
+            new_dir = add(refl, scl(r, m.fuzz));
+        }
+        atten = ld3(m.albedo);
+    } else {                                                                                     // dielectric :68-95
+#else
     if (m.type == 0) {                                                                           // lambertian :52-61
         F3 nd = add(normal, unit(rand_in_unit_sphere(g)));
         if (fabsf(nd.x) < 1e-8f && fabsf(nd.y) < 1e-8f && fabsf(nd.z) < 1e-8f) nd = normal;      // near_zero vec3.rs:69-72
@@ -276,6 +296,7 @@ __device__ __forceinline__ void scatter(const OmMaterial& m, F3 dir, F3 normal, 
         const F3 refl = reflect(dir, normal);
         new_dir = add(refl, scl(rand_in_unit_sphere(g), m.fuzz)); atten = ld3(m.albedo);
     } else {                                                                                     // dielectric :68-95
+#endif
         const bool front = dot(dir, normal) < 0.0f;
         const float rr = front ? 1.0f / m.ior : m.ior;
         const F3 n = front ? normal : neg(normal);

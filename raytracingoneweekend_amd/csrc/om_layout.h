@@ -129,6 +129,9 @@ struct OM_ALIGN16 OmAlwaysRec {
 // OM_LEAF | leaf index; b2leaves[leaf] = (first_record << 8) | count (records =
 // srecs, leaf order).  The traversal stack holds these 16-bit codes.
 #define OM_LEAF 0x8000u
+#ifndef OM_B2_DIRECT
+#define OM_B2_DIRECT 1
+#endif
 // OM_PK_SLAB: the box planes interleaved as (lo, hi) pairs per axis, b[6k + 2i] = lo_k[i],
 // b[6k + 2i + 1] = hi_k[i], so one v_pk_fma_f32 gives both slab distances of an axis.
 #ifndef OM_PK_SLAB
@@ -183,6 +186,7 @@ struct OmSceneDev {
     uint32_t n_b2nodes, n_b2leaves;
     uint32_t b2_lds_bytes;        // node bytes when they fit the LDS budget, else 0 (global nodes)
     uint32_t b2_stack;            // lane-stack entries the tree needs (its internal depth, <= 24)
+    uint32_t b2_direct;           // leaf codes are OM_LEAF | first_record << 4 | count (om_bvh.cpp), not table indices
     // BVH4 collapsed from the BVH2 (same leaf table / records / always2)
     const OmBvh4Node* b4nodes;
     uint32_t n_b4nodes;

@@ -637,6 +637,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
                        fw.b2_depth <= 24u;   // lane stack bound (om_wavefront.hip kStackDepth)
     S.n_b2nodes = b2_ok ? (uint32_t)fw.b2nodes.size() : 0u;
     S.n_b2leaves = b2_ok ? (uint32_t)fw.b2leaves.size() : 0u;
+    S.b2_direct = b2_ok ? fw.b2_direct : 0u;
     S.b2_stack = b2_ok ? fw.b2_depth : 0u;   // one push per internal level on the current path, deepest included
     const size_t b2_bytes = fw.b2nodes.size() * sizeof(OmBvh2Node) + fw.b2leaves.size() * 4u;
     S.b2_lds_bytes = (b2_ok && b2_bytes <= 40u * 1024u) ? (uint32_t)((b2_bytes + 15u) & ~(size_t)15u) : 0u;

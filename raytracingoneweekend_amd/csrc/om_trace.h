@@ -268,6 +268,12 @@ __device__ __forceinline__ void test_rec(const OmAffineTest& R, F3 o, F3 d, floa
     w.lap(LAP_REC_TEST);
 }
 
+// (first record << 8) | count of the leaf with child code `code`: straight from a direct code
+// (OM_LEAF | first << 4 | count, om_bvh.cpp), else from the leaf table.
+__device__ __forceinline__ uint32_t leaf_payload(const OmSceneDev& S, uint32_t code, const uint32_t* leaves) {
+    return S.b2_direct ? ((((code >> 4) & 0x7FFu) << 8) | (code & 15u)) : leaves[code & (OM_LEAF - 1u)];
+}
+
 // Leaf of the BVH2/BVH4: its records, tested in place.
 template <class Wk>
 __device__ __forceinline__ void test_leaf(const OmAffineTest* recs, uint32_t lf, F3 o, F3 d, float tmin, float& closest,
@@ -811,7 +817,7 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
 #endif
     for (;;) {
         if (cur & OM_LEAF) {                            // the single leaf site
-            test_leaf(recs, leaves[cur & (OM_LEAF - 1u)], o, d, tmin, closest, best, w);
+            test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
             if (sp == 0) break;
             OM_B2_POP();
             w.lap(LAP_POP);
@@ -894,7 +900,7 @@ template <int STRIDE>
 __device__ __forceinline__ void b2_enter(B2Ray& r, uint32_t c, const uint32_t* leaves, const uint16_t* stk) {
     for (;;) {
         if (!(c & OM_LEAF)) { r.cur = c; return; }
-        const uint32_t lf = leaves[c & (OM_LEAF - 1u)];
+        const uint32_t lf = leaves[c & (OM_LEAF - 1u)];        // (OM_WF_DUAL requires OM_B2_DIRECT=0)
         if (lf & 255u) { r.leaf = lf; return; }
         if (--r.sp < 0) return;
         c = stk[r.sp * STRIDE];
@@ -999,7 +1005,7 @@ __device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node
     int sp = 0;
     for (;;) {
         if (cur & OM_LEAF) {
-            test_leaf(recs, leaves[cur & (OM_LEAF - 1u)], o, d, tmin, closest, best, w);
+            test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
             if (sp == 0) break;
             --sp;
             cur = stk[sp * STRIDE];

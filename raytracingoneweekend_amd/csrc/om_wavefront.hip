@@ -126,6 +126,9 @@ constexpr uint32_t kTailDefault = 16;                             // first bounc
 #ifndef OM_WF_WAVEQ
 #define OM_WF_WAVEQ 1
 #endif
+#ifndef OM_WF_MAX_PATHS_LOG2
+#define OM_WF_MAX_PATHS_LOG2 27
+#endif
 // Bounce 0 with primary tile lists: a wave whose lanes all lie in one 8x8 tile (every wave but
 // those where partial tiles meet) reads the tile's list and records with scalar loads.
 #ifndef OM_TILES_UNIFORM
@@ -615,6 +618,9 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
 #ifndef OM_WF_DUAL
 #define OM_WF_DUAL 0
 #endif
+#if OM_WF_DUAL && OM_B2_DIRECT
+#error "OM_WF_DUAL's b2_enter reads the leaf table: build it with -DOM_B2_DIRECT=0"
+#endif
 #ifndef OM_WF_DUAL_WAVES
 #define OM_WF_DUAL_WAVES 0
 #endif
@@ -1073,7 +1079,12 @@ hipError_t ensure_events(Buffers& B, size_t n) {
 hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err) {
     const uint32_t n_px = L.n_pixels;
     if (n_px == 0 || L.P.sample_count == 0) return hipSuccess;
-    const uint64_t kMaxPaths = 1ull << 25;   // 33.5M paths per batch (~4.9 GB of queues per set)
+    // paths per batch: 2^25 (33.5M, ~4.9 GB of queues per set; 16 spp of 1080p, the measured sweet
+    // spot, §5.5), raised up to 16 spp of the frame for frames above 2M pixels, within 2^27 (~21 GB
+    // per set, two sets; MI355X has 288 GB): a 4K frame (C4, 8.3M pixels) then runs 16-spp batches
+    // like 1080p instead of 4-spp ones, whose 4x launches and 4x Stats read-modify-write per sample
+    // cost C4 ~11% in k_accumulate alone (r03)
+    const uint64_t kMaxPaths = std::min<uint64_t>(1ull << OM_WF_MAX_PATHS_LOG2, std::max<uint64_t>(1ull << 25, 16ull * n_px));
     const uint32_t want = std::max<uint32_t>(1u, std::min<uint32_t>(L.streams, (uint32_t)kMaxSets));
     const bool concurrent = !L.P.adaptive && want >= 2u && L.P.sample_count >= 2u;
     uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));

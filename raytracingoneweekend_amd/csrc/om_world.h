@@ -44,6 +44,7 @@ struct FrozenWorld {
     std::vector<OmBvh2Node> b2nodes;   // compressed BVH2 (same leaves/records as snodes)
     std::vector<uint32_t> b2leaves;    // its leaf table: (first_record << 8) | count
     uint32_t b2_depth = 0;             // its depth (stack bound)
+    uint32_t b2_direct = 0;            // 1: leaf child codes carry OM_LEAF | first_record << 4 | count (no table read)
     std::vector<OmBvh4Node> b4nodes;   // 4-wide tree collapsed from b2nodes (leaf codes index b2leaves)
     uint32_t b4_depth = 0;             // its depth
     uint32_t counts[8];

@@ -104,11 +104,17 @@ declare -A V=(
   # r03: always2 records through scalar loads (default on) or vector loads
   [a2vec]="$COMMON $DEV -DOM_A2_SCALAR=0"
   # r03: two paths per lane in the later bounces (k_bounce2), occupancy request 0 (none) / 6 / 5
-  [dual]="$COMMON $DEV -DOM_WF_DUAL=1"
+  [dual]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_B2_DIRECT=0"
   # r03: bounce 0's tile lists through vector loads only (default: scalar when the wave is one tile)
   [tilesvec]="$COMMON $DEV -DOM_TILES_UNIFORM=0"
-  [dual6]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=6"
-  [dual5]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=5"
+  # r03: one rand_in_unit_sphere loop for Lambertian and Metal lanes (default) or one per kind
+  [scat2]="$COMMON $DEV -DOM_SCATTER_SHARED_SPHERE=0"
+  # r03: leaf codes through the leaf table (default: direct first/count codes when they fit)
+  [leaftab]="$COMMON $DEV -DOM_B2_DIRECT=0"
+  # r03: 2^25 paths per batch (r02) instead of 2^27: C4's 4K frame in 4-spp batches
+  [mp25]="$COMMON $DEV -DOM_WF_MAX_PATHS_LOG2=25"
+  [dual6]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=6 -DOM_B2_DIRECT=0"
+  [dual5]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=5 -DOM_B2_DIRECT=0"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
