@@ -109,3 +109,32 @@ def test_tiles_partition_the_frame():
             allp = np.concatenate(parts)
             assert allp.size == w * h and np.unique(allp).size == w * h
             assert max(p.size for p in parts) <= shard.shard_capacity(w, h, ws)
+
+
+@pytest.mark.parametrize("W,H", [(1, 1), (7, 5), (13, 9), (53, 37), (641, 359), (3840, 2160)])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 7, 8])
+def test_tile_deal_partitions_the_frame(om, W, H, n):
+    """the product's deal (om_shard_pixels) over all ranks covers every pixel exactly
+    once, for odd frame sizes and rank counts; every shard fits om_shard_capacity, so the gather's
+    staging offsets q * capacity (om_gather_frame, om_multi_gather) never overlap; each rank's
+    pixels come in its tile order (t % n == rank, row-major tiles, lane order 8*y + x inside)."""
+    from raytracingoneweekend_amd import shard
+    cap = shard.shard_capacity(W, H, n)
+    seen = np.zeros(W * H, dtype=np.int32)
+    counts = []
+    for r in range(n):
+        pix = shard.tile_pixels(W, H, r, n)
+        counts.append(pix.size)
+        assert pix.size <= cap
+        np.add.at(seen, pix.astype(np.int64), 1)
+        x, y = pix % W, pix // W
+        tiles_x = (W + 7) // 8
+        t = (y // 8) * tiles_x + x // 8
+        assert np.all(t % n == r)
+        key = t.astype(np.int64) * 64 + (y % 8) * 8 + (x % 8)
+        assert np.all(np.diff(key) > 0)                                 # tile order, lane order inside
+    assert np.all(seen == 1)
+    assert sum(counts) == W * H and max(counts) <= cap
+    # the gather's staging layout: rank q's shard at q * cap, no overlap, all within n * cap
+    ends = [q * cap + counts[q] for q in range(n)]
+    assert all(ends[q] <= (q + 1) * cap for q in range(n))
