@@ -80,6 +80,9 @@ __device__ __forceinline__ F3 rand_in_unit_sphere(Rng& g) {                     
 #define OM_SPHERE_FAST_REJECT 0
 #endif
 // Sphere::hit (traced.rs:39-62) up to the accepted root, from the ray in local space.
+// FASTREJ: the division-free rejection below regardless of OM_SPHERE_FAST_REJECT (bounce 0's
+// tile lists, OM_TILES_FAST_REJECT: coherent waves often reject an occluded candidate together).
+template <bool FASTREJ = false>
 __device__ __forceinline__ bool sphere_root_local(F3 lo, F3 ld, float tmin, float tmax, float& root) {
     const float a = dot(ld, ld);
     const float half_b = dot(lo, ld);
@@ -88,7 +91,7 @@ __device__ __forceinline__ bool sphere_root_local(F3 lo, F3 ld, float tmin, floa
     if (disc < 0.0f) return false;
     const float sqrtd = sqrtf(disc);
     const float n1 = -half_b - sqrtd, n2 = -half_b + sqrtd;
-#if OM_SPHERE_FAST_REJECT
+    if (OM_SPHERE_FAST_REJECT || FASTREJ) {
     // Both roots provably outside [tmin, tmax] without the two correctly rounded divisions
     // (~24 VALU): for a > 0 in the normal range, n < (tmin*a)(1-2^-18) implies
     // fl(n/a) < tmin and n > (tmax*a)(1+2^-18) implies fl(n/a) > tmax, whatever the f32
@@ -100,7 +103,7 @@ __device__ __forceinline__ bool sphere_root_local(F3 lo, F3 ld, float tmin, floa
         const float lo = (tmin * a) * (1.0f - 0x1p-18f), hi = (tmax * a) * (1.0f + 0x1p-18f);
         if (n2 < lo || n1 > hi || (n1 < lo && n2 > hi)) return false;
     }
-#endif
+    }
     float r = n1 / a;
     if (r < tmin || r > tmax) {
         r = n2 / a;
@@ -109,8 +112,9 @@ __device__ __forceinline__ bool sphere_root_local(F3 lo, F3 ld, float tmin, floa
     root = r;
     return true;
 }
+template <bool FASTREJ = false>
 __device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root) {
-    return sphere_root_local(xform_p(T.w2l, o), xform_v(T.w2l, T.dz, d), tmin, tmax, root);
+    return sphere_root_local<FASTREJ>(xform_p(T.w2l, o), xform_v(T.w2l, T.dz, d), tmin, tmax, root);
 }
 // The same test for a sphere whose world-to-local block is diagonal (off-diagonal entries
 // exactly +-0: an axis-aligned scaled sphere such as random_scene's ground, main.rs:38-40).

@@ -254,7 +254,7 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
 }
 
 // One leaf record (Sphere/Cube test record, tag bit 31 = cube), brute-force tie rule.
-template <class Wk>
+template <bool FASTREJ = false, class Wk>
 __device__ __forceinline__ void test_rec(const OmAffineTest& R, F3 o, F3 d, float tmin, float& closest, int& best, Wk& w) {
     uint32_t tag;
     __builtin_memcpy(&tag, &R.pad, 4);
@@ -263,7 +263,7 @@ __device__ __forceinline__ void test_rec(const OmAffineTest& R, F3 o, F3 d, floa
     int ax;
     w.add_prim();
     w.lap(LAP_REC_WAIT);
-    const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root(R, o, d, tmin, closest, t);
+    const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root<FASTREJ>(R, o, d, tmin, closest, t);
     if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
     w.lap(LAP_REC_TEST);
 }
@@ -747,6 +747,9 @@ __device__ __forceinline__ int nonfinite_hit(const OmSceneDev& S, float& closest
 // Primary ray with a per-tile candidate list (om_tiles.h): always2, then
 // every record the conservative lens-aware frustum of its 8x8 tile can reach — the
 // brute-force loop of hits.rs:274-285 over a superset of the records it could accept.
+#ifndef OM_TILES_FAST_REJECT
+#define OM_TILES_FAST_REJECT 1
+#endif
 // UNIFORM: every lane of the wave is in tile `tile` (the caller checked it; a bounce-0 wave is one
 // 8x8 tile of one sample except where partial tiles meet), so the list and its records are read
 // with scalar loads (uniform_load) instead of vector loads.
@@ -765,7 +768,8 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
         const uint32_t* tw = (const uint32_t*)tidx;                 // u16 entries, read as the dword holding them
         for (uint32_t k = b; k < e; ++k) {
             const uint32_t pair = uniform_load(tw + (k >> 1));
-            test_rec(uniform_load(S.srecs + ((k & 1u) ? pair >> 16 : pair & 0xFFFFu)), o, d, tmin, closest, best, w);
+            test_rec<OM_TILES_FAST_REJECT>(uniform_load(S.srecs + ((k & 1u) ? pair >> 16 : pair & 0xFFFFu)), o, d, tmin,
+                                           closest, best, w);
         }
     } else {
         const uint32_t e = toff[tile + 1];

@@ -113,6 +113,8 @@ declare -A V=(
   [leaftab]="$COMMON $DEV -DOM_B2_DIRECT=0"
   # r03: 2^25 paths per batch (r02) instead of 2^27: C4's 4K frame in 4-spp batches
   [mp25]="$COMMON $DEV -DOM_WF_MAX_PATHS_LOG2=25"
+  # r03: bounce 0's tile-list sphere tests with the division-free rejection (default on)
+  [tfr0]="$COMMON $DEV -DOM_TILES_FAST_REJECT=0"
   [dual6]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=6 -DOM_B2_DIRECT=0"
   [dual5]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=5 -DOM_B2_DIRECT=0"
 )
