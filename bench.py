@@ -179,14 +179,20 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
 
     kt = L.om_kernel_times()
     timing = timing_mode != "off"
-    L.check(L.lib.om_set_timing(ctx, {"off": 0, "launch": 1, "span": 2}[timing_mode]), ctx)   # events on `stream`
+    # region (default): two HIP events on `stream` around the K render calls and nothing inside
+    # them (every call joins its side stream back to `stream`, so the pair spans all its work);
+    # span / launch: the library's own events, once per call / around every launch
+    L.check(L.lib.om_set_timing(ctx, {"off": 0, "region": 0, "launch": 1, "span": 2}[timing_mode]), ctx)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
     # ---- timed region
     ctl.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     for _ in range(steps):
         step()
+    ev1.record(stream)
     comm.gather_frame(sh.data_ptr(), W, H, frame.data_ptr(), sptr)   # RCCL: every shard to rank 0
     torch.cuda.synchronize()
     ctl.barrier()
@@ -194,6 +200,7 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
     # ---- end timed region
 
     elapsed = ctl.max(elapsed)
+    region_s = ev0.elapsed_time(ev1) / 1e3                    # device time of the K calls
     L.check(L.lib.om_get_kernel_times(ctx, C.byref(kt)), ctx)
     L.check(L.lib.om_set_timing(ctx, 0), ctx)
     host = sh.cpu().numpy().copy()
@@ -208,9 +215,6 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
     # per-launch durations (untimed): the same K steps again, production build, every launch
     # bracketed by events on its stream (om_set_timing 1) -> the rocprof-comparable average
     # launch duration and the launch concurrency inside a call; same shard, bit for bit
-    mega = kt.launches[L.KT_CLASSES.index("megakernel")] > 0     # the pipeline that actually ran (auto)
-    fam = [L.KT_CLASSES.index("megakernel")] if mega else [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
-    span_i = L.KT_CLASSES.index("megakernel" if mega else "bounce_span")
     kl = L.om_kernel_times()
     if timing:
         sh.zero_()
@@ -221,6 +225,9 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
         L.check(L.lib.om_get_kernel_times(ctx, C.byref(kl)), ctx)
         L.check(L.lib.om_set_timing(ctx, 0), ctx)
         assert np.array_equal(sh.cpu().numpy(), host), "per-launch timing changed the result"
+    mega = kl.launches[L.KT_CLASSES.index("megakernel")] > 0     # the pipeline that actually ran (auto)
+    fam = [L.KT_CLASSES.index("megakernel")] if mega else [L.KT_CLASSES.index(k) for k in BOUNCE_FAMILY]
+    span_i = L.KT_CLASSES.index("megakernel" if mega else "bounce_span")
 
     # work counting (untimed): the same K steps again with the counting build; the shard it
     # produces must equal the timed one bit for bit (counters change nothing)
@@ -247,7 +254,9 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
     launches = sum(kl.launches[i] for i in fam) if timing else 0
     roof = None
     if timing and launches:
-        span_s = kt.ms[span_i] / 1e3                               # timed region: the calls' device time
+        # the timed region's device time of the calls: the event pair (region), or the sum of the
+        # library's per-call spans (span / launch modes)
+        span_s = region_s if timing_mode == "region" else kt.ms[span_i] / 1e3
         per_launch_s = sum(kl.ms[i] for i in fam) / 1e3 / launches  # rerun: mean launch duration
         rerun_span_s = kl.ms[span_i] / 1e3
         flops = (FLOP_EXACT_TEST * ctr.prim_tests + FLOP_BOX_TEST * ctr.pre_tests + FLOP_SEGMENT * ctr.segments
@@ -306,9 +315,10 @@ def main():
     ap.add_argument("--pipeline", default="auto", choices=list(L.PIPELINES))
     ap.add_argument("--tail", type=int, default=0, help="first bounce of the persistent tail launch (0 = library default)")
     ap.add_argument("--streams", type=int, default=2, help="wavefront batches in flight per call (om_set_streams; 1 = serial)")
-    ap.add_argument("--kernel-timing", default="span", choices=["span", "launch", "off"],
-                    help="HIP events in the timed region: span = once around each call's bounce kernels "
-                         "(2 events/step, default), launch = around every launch (per-kernel breakdown)")
+    ap.add_argument("--kernel-timing", default="region", choices=["region", "span", "launch", "off"],
+                    help="HIP events in the timed region: region = one pair around all K calls (default), "
+                         "span = the library's pair around each call's bounce kernels (2 events/step), "
+                         "launch = around every launch (per-kernel breakdown); off = none and no roofline")
     ap.add_argument("--primary-lists", default="auto", choices=["off", "auto", "on"],
                     help="bounce-0 per-tile candidate lists (DESIGN.md §5.10); auto = when they average <= 12")
     ap.add_argument("--no-cpu-baseline", action="store_true",
@@ -336,14 +346,14 @@ def main():
         extras = {}
         for name in ("C2", "C3"):
             c = CONFIGS[name]
-            e = run_config(name, args, ctl, local_rank, c["spp"] // args.spp_per_step, 1, args.spp_per_step, "span")
+            e = run_config(name, args, ctl, local_rank, c["spp"] // args.spp_per_step, 1, args.spp_per_step, "region")
             extras[name] = {"metric": "Msamples/s", "value": e["value"], "ms_per_step": round(e["elapsed_s"] / e["steps"] * 1e3, 4),
                             "workload": workload(name, e), "pipeline": "megakernel" if e["mega"] else "wavefront",
                             "roofline": e["roofline"], "work": e["work"],
                             "cpu_baseline": cpu_baseline(name, min(8.0, args.cpu_budget))}
         # C4's 4K frame at N=1: 8 steps of 32 spp (256 of the config's 4096 spp; the full frame is
         # the multi-GPU run, --config C4), so the driver's line exercises the 3840x2160 frame too
-        e = run_config("C4", args, ctl, local_rank, 8, 1, args.spp_per_step, "span")
+        e = run_config("C4", args, ctl, local_rank, 8, 1, args.spp_per_step, "region")
         extras["C4"] = {"metric": "Msamples/s", "value": e["value"], "ms_per_step": round(e["elapsed_s"] / e["steps"] * 1e3, 4),
                         "workload": workload("C4", e) + " (N=1 leg of the 8-GPU config: 256 of its 4096 spp)",
                         "pipeline": "megakernel" if e["mega"] else "wavefront",

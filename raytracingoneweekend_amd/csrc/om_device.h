@@ -116,6 +116,35 @@ template <bool FASTREJ = false>
 __device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root) {
     return sphere_root_local<FASTREJ>(xform_p(T.w2l, o), xform_v(T.w2l, T.dz, d), tmin, tmax, root);
 }
+// Sphere::hit split in two (bounce 0's paired tile tests, om_trace.h): the expensive part (the
+// transform, the quadratic, sqrt and both quotients) does not depend on tmax, only the root
+// choice does, so two candidates' expensive parts can run interleaved and their choices in
+// order.  n2 / a is computed even when the near root is accepted (the reference skips it);
+// each quotient is the same IEEE operation, so the accepted root is bit-identical.
+struct SpherePre { float r1, r2; bool ok; };
+__device__ __forceinline__ SpherePre sphere_pre(const OmAffineTest& T, F3 o, F3 d) {
+    const F3 lo = xform_p(T.w2l, o), ld = xform_v(T.w2l, T.dz, d);
+    const float a = dot(ld, ld);
+    const float half_b = dot(lo, ld);
+    const float c = dot(lo, lo) - 1.0f;
+    const float disc = half_b * half_b - a * c;
+    SpherePre p;
+    p.ok = !(disc < 0.0f);
+    const float sqrtd = sqrtf(disc);
+    p.r1 = (-half_b - sqrtd) / a;
+    p.r2 = (-half_b + sqrtd) / a;
+    return p;
+}
+__device__ __forceinline__ bool sphere_pick(const SpherePre& p, float tmin, float tmax, float& root) {
+    if (!p.ok) return false;
+    float r = p.r1;
+    if (r < tmin || r > tmax) {
+        r = p.r2;
+        if (r < tmin || r > tmax) return false;
+    }
+    root = r;
+    return true;
+}
 // The same test for a sphere whose world-to-local block is diagonal (off-diagonal entries
 // exactly +-0: an axis-aligned scaled sphere such as random_scene's ground, main.rs:38-40).
 // Each dropped term of ((m0*x + m1*y) + m2*z) + m3 is a signed zero, and adding a signed zero

@@ -345,6 +345,7 @@ __device__ __forceinline__ int traced_sbvh(const OmSceneDev& S, const OmSkipNode
 struct MarchedArrays {
     static constexpr uint32_t KS = 0u, KB = 0u, KT = 0u;      // 0: unbounded
     static constexpr bool INDEXED = true;
+    static constexpr bool RELOAD = false;
     const OmMSphere* s; const OmMBox* b; const OmMTorus* t;
     uint32_t ns, nb, nt;
     __device__ explicit MarchedArrays(const OmSceneDev& S)
@@ -354,6 +355,7 @@ template <uint32_t KS_, uint32_t KB_, uint32_t KT_>
 struct MarchedRegs {
     static constexpr uint32_t KS = KS_, KB = KB_, KT = KT_;
     static constexpr bool INDEXED = false;
+    static constexpr bool RELOAD = false;
     OmMSphere s[KS]; OmMBox b[KB]; OmMTorus t[KT];
     uint32_t ns, nb, nt;
     __device__ explicit MarchedRegs(const OmSceneDev& S) : ns(S.n_msph), nb(S.n_mbox), nt(S.n_mtor) {
@@ -386,6 +388,7 @@ template <uint32_t NS, uint32_t NB, uint32_t NT>
 struct MarchedExact {
     static constexpr uint32_t KS = NS, KB = NB, KT = NT;      // for_objects: unrolled (0: no loop)
     static constexpr bool INDEXED = false;
+    static constexpr bool RELOAD = false;
     static constexpr uint32_t ns = NS, nb = NB, nt = NT;
     OmMSphere s[NS ? NS : 1]; OmMBox b[NB ? NB : 1]; MTorusSdf t[NT ? NT : 1];
     __device__ explicit MarchedExact(const OmSceneDev& S) {
@@ -397,6 +400,29 @@ struct MarchedExact {
         for (uint32_t i = 0; i < NT; ++i) t[i].load(S.mtor[i]);
     }
     __host__ __device__ static bool matches(uint32_t n_s, uint32_t n_b, uint32_t n_t) { return n_s == NS && n_b == NB && n_t == NT; }
+};
+
+// The same exact-count view with the parameters staged in LDS (the north_star's "LDS-staged SDF
+// params"; OM_WF_MARCH_EXACT = 2 selects it for k_march): one workgroup-wide copy,
+// every step reads them with broadcast ds_reads at constant offsets.
+template <uint32_t NS, uint32_t NB, uint32_t NT>
+struct MarchedExactLds {
+    static constexpr uint32_t KS = NS, KB = NB, KT = NT;
+    static constexpr bool INDEXED = false;
+    // re-read every step (a compiler-only fence in nearest_marched): hoisted out of the march loop
+    // the parameters would sit in VGPRs (64 + 23 spilled) instead of LDS
+    static constexpr bool RELOAD = true;
+    static constexpr uint32_t ns = NS, nb = NB, nt = NT;
+    struct Block { OmMSphere s[NS ? NS : 1]; OmMBox b[NB ? NB : 1]; MTorusSdf t[NT ? NT : 1]; };
+    const OmMSphere* s; const OmMBox* b; const MTorusSdf* t;
+    // every thread of the block calls it (it ends with a barrier)
+    __device__ MarchedExactLds(const OmSceneDev& S, Block* lds) : s(lds->s), b(lds->b), t(lds->t) {
+        const uint32_t i = threadIdx.x;
+        if (i < NS) lds->s[i] = S.msph[i];
+        else if (i < NS + NB) lds->b[i - NS] = S.mbox[i - NS];
+        else if (i < NS + NB + NT) lds->t[i - NS - NB].load(S.mtor[i - NS - NB]);
+        __syncthreads();
+    }
 };
 
 // for (i < n) body(i): unrolled over the register view's bound, a plain loop otherwise (K = 0:
@@ -496,6 +522,7 @@ __device__ __forceinline__ float nearest_marched_pf(const MarchedArrays& m, F3 p
 template <class M>
 __device__ __forceinline__ float nearest_marched(const M& m, F3 p, int& bk, uint32_t& bi) {
     if constexpr (OM_MARCH_PREFETCH && M::INDEXED) return nearest_marched_pf(m, p, bk, bi);
+    if constexpr (M::RELOAD) __atomic_signal_fence(__ATOMIC_SEQ_CST);
     float best = INFINITY;
     bk = -1; bi = 0;
     for_objects<M::KS>(m.ns, [&](uint32_t i) {
@@ -750,6 +777,9 @@ __device__ __forceinline__ int nonfinite_hit(const OmSceneDev& S, float& closest
 #ifndef OM_TILES_FAST_REJECT
 #define OM_TILES_FAST_REJECT 1
 #endif
+#ifndef OM_TILES_PAIRED
+#define OM_TILES_PAIRED 0      // measured: -0.4% on C1
+#endif
 // UNIFORM: every lane of the wave is in tile `tile` (the caller checked it; a bounce-0 wave is one
 // 8x8 tile of one sample except where partial tiles meet), so the list and its records are read
 // with scalar loads (uniform_load) instead of vector loads.
@@ -766,11 +796,34 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
     if constexpr (UNIFORM) {
         const uint32_t b = uniform_load(toff + tile), e = uniform_load(toff + tile + 1);
         const uint32_t* tw = (const uint32_t*)tidx;                 // u16 entries, read as the dword holding them
-        for (uint32_t k = b; k < e; ++k) {
+        auto rec_at = [&](uint32_t k) {
             const uint32_t pair = uniform_load(tw + (k >> 1));
-            test_rec<OM_TILES_FAST_REJECT>(uniform_load(S.srecs + ((k & 1u) ? pair >> 16 : pair & 0xFFFFu)), o, d, tmin,
-                                           closest, best, w);
+            return (k & 1u) ? pair >> 16 : pair & 0xFFFFu;
+        };
+        uint32_t k = b;
+#if OM_TILES_PAIRED
+        // two sphere candidates at a time: their tmax-independent parts interleaved (two
+        // dependency chains in flight: bounce 0 stalls on issue, not memory), the root choices
+        // and the acceptances in list order (each with the closest the previous one left)
+        for (; k + 1u < e; k += 2u) {
+            const OmAffineTest R0 = uniform_load(S.srecs + rec_at(k)), R1 = uniform_load(S.srecs + rec_at(k + 1u));
+            uint32_t t0, t1;
+            __builtin_memcpy(&t0, &R0.pad, 4);
+            __builtin_memcpy(&t1, &R1.pad, 4);
+            if ((t0 | t1) >> 31) {                                   // a cube: the plain tests
+                test_rec(R0, o, d, tmin, closest, best, w);
+                test_rec(R1, o, d, tmin, closest, best, w);
+                continue;
+            }
+            const SpherePre p0 = sphere_pre(R0, o, d), p1 = sphere_pre(R1, o, d);
+            float t;
+            w.add_prim();
+            if (sphere_pick(p0, tmin, closest, t) && (t < closest || (int)t0 > best)) { closest = t; best = (int)t0; }
+            w.add_prim();
+            if (sphere_pick(p1, tmin, closest, t) && (t < closest || (int)t1 > best)) { closest = t; best = (int)t1; }
         }
+#endif
+        for (; k < e; ++k) test_rec<OM_TILES_FAST_REJECT>(uniform_load(S.srecs + rec_at(k)), o, d, tmin, closest, best, w);
     } else {
         const uint32_t e = toff[tile + 1];
         for (uint32_t k = toff[tile]; k < e; ++k) test_rec(S.srecs[tidx[k]], o, d, tmin, closest, best, w);

@@ -160,14 +160,16 @@ __host__ __device__ inline uint32_t hyb_nodes(const OmSceneDev& S) {
 #ifndef OM_WF_MARCH_REGS
 #define OM_WF_MARCH_REGS 0
 #endif
-// k_march instance for a marched set of exactly C2's shape (2 spheres, 1 box, 1 torus: S-marched):
-// MarchedExact, the SDF-only fields copied to SGPRs once per workgroup and every march step
-// unrolled with no count guards.  Traced parts TR_BRUTE / TR_BVH2_LDS only.
+// k_march instance for a marched set of exactly C2's shape (2 spheres, 1 box, 1 torus: S-marched),
+// every march step unrolled with no count guards: 2 (default) the SDF-only fields
+// staged in LDS once per workgroup (MarchedExactLds), 1 copied to SGPRs (MarchedExact; C2 -1.4%),
+// 0 the arrays view.  Traced parts TR_BRUTE / TR_BVH2_LDS only.
 #ifndef OM_WF_MARCH_EXACT
-#define OM_WF_MARCH_EXACT 1
+#define OM_WF_MARCH_EXACT 2
 #endif
 using MarchedC2 = MarchedExact<2, 1, 1>;
-enum { MV_ARRAYS = 0, MV_SMALL = 1, MV_EXACT_C2 = 2 };
+using MarchedC2Lds = MarchedExactLds<2, 1, 1>;
+enum { MV_ARRAYS = 0, MV_SMALL = 1, MV_EXACT_C2 = 2, MV_EXACT_C2_LDS = 3 };
 template <int TR>
 __host__ __device__ constexpr bool exact_view_built() { return OM_WF_MARCH_EXACT && (TR == TR_BRUTE || TR == TR_BVH2_LDS); }
 // k_march refills its idle lanes once at least this many of a wave's 64 wait.
@@ -792,7 +794,10 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_march(OmSceneDev S, OmPa
     __syncthreads();
     const Tracer T = stage_scene<TR>(S);
     WorkT<COUNT> w;
-    if constexpr (VIEW == MV_EXACT_C2) march_lanes<TR, COUNT>(S, P, T, MarchedC2(S), in, seg0, n, next, hit, w);
+    if constexpr (VIEW == MV_EXACT_C2_LDS) {
+        __shared__ MarchedC2Lds::Block mblock;
+        march_lanes<TR, COUNT>(S, P, T, MarchedC2Lds(S, &mblock), in, seg0, n, next, hit, w);
+    } else if constexpr (VIEW == MV_EXACT_C2) march_lanes<TR, COUNT>(S, P, T, MarchedC2(S), in, seg0, n, next, hit, w);
     else if constexpr (VIEW == MV_SMALL) march_lanes<TR, COUNT>(S, P, T, MarchedSmall(S), in, seg0, n, next, hit, w);
     else march_lanes<TR, COUNT>(S, P, T, MarchedArrays(S), in, seg0, n, next, hit, w);
     if (COUNT) {
@@ -995,8 +1000,12 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
             const bool exact = MarchedC2::matches(L.S.n_msph, L.S.n_mbox, L.S.n_mtor);
             if constexpr (exact_view_built<TR>()) {
                 if (exact) {
-                    hipLaunchKernelGGL((k_march<TR, COUNT, MV_EXACT_C2>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin,
-                                       B.hit, L.counters);
+                    if (OM_WF_MARCH_EXACT == 2)
+                        hipLaunchKernelGGL((k_march<TR, COUNT, MV_EXACT_C2_LDS>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G,
+                                           in, cin, B.hit, L.counters);
+                    else
+                        hipLaunchKernelGGL((k_march<TR, COUNT, MV_EXACT_C2>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in,
+                                           cin, B.hit, L.counters);
                     goto launched;
                 }
             }

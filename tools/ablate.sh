@@ -96,6 +96,8 @@ declare -A V=(
   [tprio0]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0"
   # r03: C2's k_march with the SDF-only exact register view (default on) or the arrays view
   [noexact]="$COMMON $DEV -DOM_WF_MARCH_EXACT=0"
+  [exactlds]="$COMMON $DEV -DOM_WF_MARCH_EXACT=2"
+  [exactsgpr]="$COMMON $DEV -DOM_WF_MARCH_EXACT=1"
   # r03: diagnostic build, per-phase wave cycles (tools/phase_stamps.py)
   [phase]="$COMMON $DEV -DOM_PHASE_STAMPS=1"
   [phase2]="$COMMON $DEV -DOM_PHASE_STAMPS=2"
@@ -115,6 +117,10 @@ declare -A V=(
   [mp25]="$COMMON $DEV -DOM_WF_MAX_PATHS_LOG2=25"
   # r03: bounce 0's tile-list sphere tests with the division-free rejection (default on)
   [tfr0]="$COMMON $DEV -DOM_TILES_FAST_REJECT=0"
+  # r03: bounce 0's tile candidates: sphere pairs interleaved (measured -0.4%, default off)
+  [tpair1]="$COMMON $DEV -DOM_TILES_PAIRED=1"
+  # r02 knob, run at last: bounce 0's occupancy request 7 / 6 waves per SIMD (default 8)
+  [first7b]="$COMMON $DEV -DOM_WF_WAVES_FIRST=7"
   [dual6]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=6 -DOM_B2_DIRECT=0"
   [dual5]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=5 -DOM_B2_DIRECT=0"
 )
