@@ -115,6 +115,10 @@ constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segme
 #ifndef OM_WF_TAIL_PRIO
 #define OM_WF_TAIL_PRIO 1
 #endif
+// With async tails: the bounce from which a batch moves to its tail stream (0: only the tail).
+#ifndef OM_WF_DRAIN_AT
+#define OM_WF_DRAIN_AT 0
+#endif
 constexpr uint32_t kTailSpbAsync = OM_WF_TAIL_SPB_ASYNC;
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
 // Work distribution inside a bounce workgroup.  1 (default): every wave takes 64-path
@@ -1024,12 +1028,22 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         if (T.ev) { (void)hipEventRecord(T.ev, st); (void)hipStreamWaitEvent(T.st, T.ev, 0); }
         return launches;
     }
+    Tail TT = T;
     for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
         const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
         const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
         if (bounce > 0 && bounce >= tail_at) {
-            launch_tail<TR, COUNT, MARCH>(L, B, G, in, cin, lds, st, T, tm, each);
+            launch_tail<TR, COUNT, MARCH>(L, B, G, in, cin, lds, st, TT, tm, each);
             return launches + 1u;
+        }
+        // async drain (OM_WF_DRAIN_AT, with async tails): from this bounce on, the batch's light
+        // late bounces, its tail and its accumulate run on the tail stream, so the main stream
+        // already starts the next batch's heavy bounces on another queue set
+        if (OM_WF_DRAIN_AT > 0 && TT.ev && bounce == (uint32_t)OM_WF_DRAIN_AT) {
+            (void)hipEventRecord(TT.ev, st);
+            (void)hipStreamWaitEvent(TT.st, TT.ev, 0);
+            st = TT.st;
+            TT.ev = nullptr;
         }
         uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
         const int ti = each ? tm.begin(st) : -1;
@@ -1047,7 +1061,7 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         tm.end(ti, bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE, st);
         ++launches;
     }
-    if (T.ev) { (void)hipEventRecord(T.ev, st); (void)hipStreamWaitEvent(T.st, T.ev, 0); }
+    if (TT.ev) { (void)hipEventRecord(TT.ev, st); (void)hipStreamWaitEvent(TT.st, TT.ev, 0); }
     return launches;
 }
 

@@ -94,6 +94,11 @@ declare -A V=(
   [memclause]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-memory-clause"
   [bias0]="$COMMON $DEV -mllvm -amdgpu-schedule-metric-bias=0"
   [tprio0]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0"
+  # r03: async drain: a batch's bounces >= K, tail and accumulate on its tail stream (4 queue sets)
+  [drain4]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0 -DOM_WF_DRAIN_AT=4"
+  [drain6]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0 -DOM_WF_DRAIN_AT=6"
+  [drain8]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=0 -DOM_WF_DRAIN_AT=8"
+  [drain6p]="$COMMON $DEV -DOM_WF_ASYNC_TAIL=1 -DOM_WF_TAIL_PRIO=1 -DOM_WF_DRAIN_AT=6"
   # r03: C2's k_march with the SDF-only exact register view (default on) or the arrays view
   [noexact]="$COMMON $DEV -DOM_WF_MARCH_EXACT=0"
   [exactlds]="$COMMON $DEV -DOM_WF_MARCH_EXACT=2"
