@@ -4,8 +4,8 @@ Workload (config C1, BASELINE.json configs[1]): the S-traced random_scene (main.
 minus the torus block, om-rng scene seed 0x5EED), camera of main.rs:136-142, 1920x1080,
 max_depth 50, tmin 0.001, tmax 100, fixed spp (adaptive off).  One STEP = one progressive
 pass of SPP_PER_STEP samples over every pixel this rank owns, accumulated into the
-per-pixel Stats in HBM (render_thread.rs:176-199, batched).  16 steps of 32 spp at N=1 =
-the full 512-spp frame; the library runs each step as two concurrent 16-spp batches
+per-pixel Stats in HBM (render_thread.rs:176-199, batched).  4 steps of 128 spp at N=1 =
+the full 512-spp frame; the library runs each step as 16-spp batches, two in flight
 (om_set_streams).
 
 Every rank (N = 1 included) goes through the product's multi-GPU path: its
@@ -44,7 +44,9 @@ from raytracingoneweekend_amd import _lib as L  # noqa: E402
 from raytracingoneweekend_amd import shard  # noqa: E402
 
 MAX_DEPTH, TMIN, TMAX, SEED, SCENE_SEED = 50, 0.001, 100.0, 1, 0x5EED
-SPP_PER_STEP = 32
+# 128 spp per call: 8 batches of 16 spp on two streams; a call boundary drains both batches, so
+# fewer, larger calls measured +0.8% over 32 spp per call (profiles/r03_v7/ab_drain_ab*_C1.jsonl, base rows)
+SPP_PER_STEP = 128
 # BASELINE.json configs: C1 is the metric's workload (the default line); C2/C3 ride along in
 # the line's `configs` at N=1; C4 is the 4K frame of the multi-GPU config (--config C4).
 CONFIGS = {
@@ -308,7 +310,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", default="C1", choices=[c for c in CONFIGS if c != "C0"])
-    ap.add_argument("--steps", type=int, default=None, help="default: the config's spp / spp-per-step (C1: 16)")
+    ap.add_argument("--steps", type=int, default=None, help="default: the config's spp / spp-per-step (C1: 4)")
     ap.add_argument("--spp-per-step", type=int, default=SPP_PER_STEP, help="samples per pixel per step (one render call)")
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--kernel", default="auto", choices=list(L.KERNELS))
@@ -351,9 +353,9 @@ def main():
                             "workload": workload(name, e), "pipeline": "megakernel" if e["mega"] else "wavefront",
                             "roofline": e["roofline"], "work": e["work"],
                             "cpu_baseline": cpu_baseline(name, min(8.0, args.cpu_budget))}
-        # C4's 4K frame at N=1: 8 steps of 32 spp (256 of the config's 4096 spp; the full frame is
-        # the multi-GPU run, --config C4), so the driver's line exercises the 3840x2160 frame too
-        e = run_config("C4", args, ctl, local_rank, 8, 1, args.spp_per_step, "region")
+        # C4's 4K frame at N=1: 256 of the config's 4096 spp (the full frame is the multi-GPU run,
+        # --config C4), so the driver's line exercises the 3840x2160 frame too
+        e = run_config("C4", args, ctl, local_rank, max(1, 256 // args.spp_per_step), 1, args.spp_per_step, "region")
         extras["C4"] = {"metric": "Msamples/s", "value": e["value"], "ms_per_step": round(e["elapsed_s"] / e["steps"] * 1e3, 4),
                         "workload": workload("C4", e) + " (N=1 leg of the 8-GPU config: 256 of its 4096 spp)",
                         "pipeline": "megakernel" if e["mega"] else "wavefront",
