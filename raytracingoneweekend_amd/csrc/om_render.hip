@@ -277,7 +277,7 @@ struct om_ctx {
     std::vector<float> srec_box;
     uint64_t world_gen = 0;
     int primary_lists = OM_PRIMARY_LISTS_AUTO;
-    DevBuf tile_off, tile_idx;
+    DevBuf tile_off, tile_idx, tile_tnear;
     bool tiles_valid = false, tiles_use = false;
     om_camera tiles_cam{};
     uint32_t tiles_w = 0, tiles_h = 0;
@@ -292,7 +292,7 @@ struct om_ctx {
         for (auto& b : scene_bufs) b.release();
         for (auto& j : jitters) j.buf.release();
         counters.release(); stats.release(); pixels.release(); frame_list.release();
-        view_scratch.release(); view_rgb.release(); tile_off.release(); tile_idx.release();
+        view_scratch.release(); view_rgb.release(); tile_off.release(); tile_idx.release(); tile_tnear.release();
         wf.release();
         timer.release();
         if (progress_host) (void)hipHostFree(progress_host);
@@ -422,10 +422,13 @@ om_status ensure_tile_lists(om_ctx* c, const om_camera* cam, uint32_t W, uint32_
             om_status s = ensure(c, c->tile_off, tl.off.size() * 4u);
             // +1 entry: the uniform (scalar) reader loads whole dwords (traced_tiles<true>, om_trace.h)
             if (s == OM_OK) s = ensure(c, c->tile_idx, (tl.idx.size() + 2u) * 2u);
+            if (s == OM_OK) s = ensure(c, c->tile_tnear, std::max<size_t>(tl.tnear.size(), 1u) * 4u);
             if (s != OM_OK) return s;
             OM_HIP(c, hipStreamSynchronize(stream));        // the previous lists may still be read
             OM_HIP(c, hipMemcpy(c->tile_off.p, tl.off.data(), tl.off.size() * 4u, hipMemcpyHostToDevice));
             if (!tl.idx.empty()) OM_HIP(c, hipMemcpy(c->tile_idx.p, tl.idx.data(), tl.idx.size() * 2u, hipMemcpyHostToDevice));
+            if (!tl.tnear.empty())
+                OM_HIP(c, hipMemcpy(c->tile_tnear.p, tl.tnear.data(), tl.tnear.size() * 4u, hipMemcpyHostToDevice));
         }
         c->tiles_valid = true; c->tiles_gen = c->world_gen; c->tiles_w = W; c->tiles_h = H; c->tiles_cam = *cam;
         c->tiles_avg = ok ? tl.avg_per_pixel : -1.0;
@@ -498,11 +501,14 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         L.tail_bounce = c->tail_bounce;
         L.streams = c->wf_streams;
         L.timer = &c->timer;
-        L.tile_off = nullptr; L.tile_idx = nullptr;
+        L.tile_off = nullptr; L.tile_idx = nullptr; L.tile_tnear = nullptr;
         L.progress_host = c->progress_host;
         if (mode == OM_KERNEL_BVH2 && c->scene.n_b2nodes) {
             if ((s = ensure_tile_lists(c, cam, p->width, p->height, stream)) != OM_OK) return s;
-            if (c->tiles_use) { L.tile_off = (const uint32_t*)c->tile_off.p; L.tile_idx = (const uint16_t*)c->tile_idx.p; }
+            if (c->tiles_use) {
+                L.tile_off = (const uint32_t*)c->tile_off.p; L.tile_idx = (const uint16_t*)c->tile_idx.p;
+                L.tile_tnear = (const float*)c->tile_tnear.p;
+            }
         }
         L.trace_mode = mode == OM_KERNEL_BRUTE ? MODE_BRUTE : mode == OM_KERNEL_CULLED ? MODE_CULLED
                      : mode == OM_KERNEL_BVH ? MODE_BVH : mode == OM_KERNEL_BVH2 ? 6

@@ -46,6 +46,23 @@ bool build(const std::vector<float>& srec_box, const om_camera& cam, uint32_t W,
     const double wm1 = (double)(W - 1u), hm1 = (double)(H - 1u);
     struct Rect { uint32_t x0, x1, y0, y1; };
     std::vector<Rect> rect(nrec);
+    // Early-out bound (traced_tiles<true>): a primary ray starts at a lens point
+    // L (|L - O| <= R) with a unit direction, so it reaches the box no earlier than
+    // t = dist(O, box) - R.  Margins: 1e-5 relative + 1e-4 for the f32 ray set-up and root.
+    out.tnear.assign(nrec, 0.0f);
+    for (size_t r = 0; r < nrec; ++r) {
+        const float* b = &srec_box[6 * r];
+        double dd = 0.0;
+        const double o[3] = {O.x, O.y, O.z};
+        for (int a = 0; a < 3; ++a) {
+            const double e = std::max({(double)b[a] - o[a], 0.0, o[a] - (double)b[3 + a]});
+            dd += e * e;
+        }
+        const double t = (std::sqrt(dd) - R) * (1.0 - 1e-5) - 1e-4;
+        float f = t > 0.0 ? (float)t : 0.0f;
+        if ((double)f > t) f = std::nextafter(f, -INFINITY);
+        out.tnear[r] = std::isfinite(f) && f > 0.0f ? f : 0.0f;
+    }
     std::vector<uint32_t> cnt(ntiles, 0u);
     for (size_t r = 0; r < nrec; ++r) {
         const float* b = &srec_box[6 * r];
@@ -116,6 +133,9 @@ bool build(const std::vector<float>& srec_box, const om_camera& cam, uint32_t W,
         for (uint32_t y = q.y0; y <= q.y1 && q.x0 <= q.x1; ++y)
             for (uint32_t x = q.x0; x <= q.x1; ++x) out.idx[pos[y * tx + x]++] = (uint16_t)r;
     }
+    for (uint32_t t = 0; t < ntiles; ++t)                                  // nearest first (the early-out)
+        std::stable_sort(out.idx.begin() + out.off[t], out.idx.begin() + out.off[t + 1],
+                         [&](uint16_t a, uint16_t b) { return out.tnear[a] < out.tnear[b]; });
     return true;
 }
 

@@ -16,7 +16,8 @@ namespace omt {
 
 struct TileLists {
     std::vector<uint32_t> off;   // tiles + 1 prefix offsets into idx
-    std::vector<uint16_t> idx;   // srec indices
+    std::vector<uint16_t> idx;   // srec indices, each tile's sorted by tnear (ascending)
+    std::vector<float> tnear;    // per srec: a lower bound of the t at which any primary ray can reach its box
     double avg_per_pixel = 0.0;  // mean list length seen by a pixel
 };
 

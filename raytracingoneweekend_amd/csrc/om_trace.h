@@ -783,9 +783,16 @@ __device__ __forceinline__ int nonfinite_hit(const OmSceneDev& S, float& closest
 // UNIFORM: every lane of the wave is in tile `tile` (the caller checked it; a bounce-0 wave is one
 // 8x8 tile of one sample except where partial tiles meet), so the list and its records are read
 // with scalar loads (uniform_load) instead of vector loads.
+// tnear (UNIFORM): the lists are sorted by a lower bound of the t at which any primary ray can
+// reach the record's box (om_tiles.cpp); once every lane's closest is below the next record's
+// bound, that record and all later ones would be rejected (root >= bound > closest = tmax), so
+// the wave stops (OM_TILES_EARLY_OUT).  NaN closest keeps testing.
+#ifndef OM_TILES_EARLY_OUT
+#define OM_TILES_EARLY_OUT 1
+#endif
 template <bool UNIFORM = false, class Wk>
 __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t* toff, const uint16_t* tidx, uint32_t tile,
-                                            F3 o, F3 d, float tmin, float& closest, Wk& w) {
+                                            F3 o, F3 d, float tmin, float& closest, Wk& w, const float* tnear = nullptr) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
     const float ix = inv_dir(d.x);
@@ -823,7 +830,11 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
             if (sphere_pick(p1, tmin, closest, t) && (t < closest || (int)t1 > best)) { closest = t; best = (int)t1; }
         }
 #endif
-        for (; k < e; ++k) test_rec<OM_TILES_FAST_REJECT>(uniform_load(S.srecs + rec_at(k)), o, d, tmin, closest, best, w);
+        for (; k < e; ++k) {
+            const uint32_t r = rec_at(k);
+            if (OM_TILES_EARLY_OUT && tnear && __ballot(!(closest < uniform_load(tnear + r))) == 0) break;
+            test_rec<OM_TILES_FAST_REJECT>(uniform_load(S.srecs + r), o, d, tmin, closest, best, w);
+        }
     } else {
         const uint32_t e = toff[tile + 1];
         for (uint32_t k = toff[tile]; k < e; ++k) test_rec(S.srecs[tidx[k]], o, d, tmin, closest, best, w);

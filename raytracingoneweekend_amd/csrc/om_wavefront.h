@@ -89,6 +89,7 @@ struct Launch {
     Timer* timer;                // per-launch event timing (may be off)
     const uint32_t* tile_off;    // primary-ray candidate lists per 8x8 tile (null = traverse the BVH)
     const uint16_t* tile_idx;
+    const float* tile_tnear;     // per leaf record: lower bound of a primary ray's t to its box (lists sorted by it)
     unsigned long long* progress_host;   // om_progress word (pinned host) or null; device side counters[OMC_PROGRESS]
 };
 

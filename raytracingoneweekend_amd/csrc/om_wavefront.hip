@@ -310,6 +310,7 @@ struct Gen {
     uint32_t done;               // samples of the call before this batch (with n0)
     const uint32_t* tile_off;    // primary-ray candidate lists (null: traverse)
     const uint16_t* tile_idx;
+    const float* tile_tnear;
 };
 
 // A path between bounces: ray_color's loop state (render_thread.rs:128-143).
@@ -543,7 +544,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
                     // a wave within one tile reads its list with scalar loads
                     const uint32_t t0 = __builtin_amdgcn_readfirstlane(tile);
                     if (__ballot(tile != t0) == 0)
-                        best = traced_tiles<true>(S, R.tile_off, R.tile_idx, t0, p.o, p.d, P.tmin, closest, w);
+                        best = traced_tiles<true>(S, R.tile_off, R.tile_idx, t0, p.o, p.d, P.tmin, closest, w, R.tile_tnear);
                     else
 #endif
                         best = traced_tiles(S, R.tile_off, R.tile_idx, tile, p.o, p.d, P.tmin, closest, w);
@@ -1149,7 +1150,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     Gen R;
     R.C = L.C; R.jitter = L.jitter; R.stats = L.stats; R.pixels = L.pixels; R.n_pixels = n_px;
     R.by_pixel = L.stats_by_pixel ? 1u : 0u;
-    R.tile_off = L.tile_off; R.tile_idx = L.tile_idx;
+    R.tile_off = L.tile_off; R.tile_idx = L.tile_idx; R.tile_tnear = L.tile_tnear;
     R.n0 = nullptr; R.done = 0;
     hipStream_t streams[kMaxSets] = {st, st, st, st};
     Timer& tm = *L.timer;

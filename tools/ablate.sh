@@ -122,6 +122,8 @@ declare -A V=(
   [mp25]="$COMMON $DEV -DOM_WF_MAX_PATHS_LOG2=25"
   # r03: bounce 0's tile-list sphere tests with the division-free rejection (default on)
   [tfr0]="$COMMON $DEV -DOM_TILES_FAST_REJECT=0"
+  # r03: bounce 0's depth-sorted tile lists without the wave early-out
+  [teo0]="$COMMON $DEV -DOM_TILES_EARLY_OUT=0"
   # r03: bounce 0's tile candidates: sphere pairs interleaved (measured -0.4%, default off)
   [tpair1]="$COMMON $DEV -DOM_TILES_PAIRED=1"
   # r02 knob, run at last: bounce 0's occupancy request 7 / 6 waves per SIMD (default 8)
