@@ -50,6 +50,14 @@ void Buffers::release() {
     n0 = nullptr; n0_cap = 0;
     for (auto& st : side) { if (st) (void)hipStreamDestroy(st); st = nullptr; }
     for (auto& st : tail) { if (st) (void)hipStreamDestroy(st); st = nullptr; }
+    if (acc) (void)hipStreamDestroy(acc);
+    acc = nullptr;
+    for (int k = 0; k < kMaxSets; ++k) {
+        if (alt_res[k]) (void)hipFree(alt_res[k]);
+        if (alt_id[k]) (void)hipFree(alt_id[k]);
+        alt_res[k] = nullptr; alt_id[k] = nullptr;
+    }
+    alt_cap = 0;
     for (auto e : ev) (void)hipEventDestroy(e);
     ev.clear();
     cap = 0; counts_n = 0; nsets = 0;
@@ -119,8 +127,40 @@ constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segme
 #ifndef OM_WF_DRAIN_AT
 #define OM_WF_DRAIN_AT 0
 #endif
+// Concurrent batches: 1 runs every k_accumulate on the context's accumulate stream with two
+// result buffers per queue set, so a stream starts its next batch right after its tail instead
+// of waiting for its own accumulate, which waits for the other stream's (sample order): that
+// chain held the two streams in lockstep, both draining at once (r03 kernel trace).
+#ifndef OM_WF_ACC_STREAM
+#define OM_WF_ACC_STREAM 0
+#endif
+// Late bounces (b >= OM_WF_LATE_GLOBAL, 0: never) of a world whose BVH2 sits in LDS read its nodes
+// through the caches instead of staging them: a late-bounce workgroup traces a chunk or two per
+// wave, for which the 19 KB copy into LDS (and its barrier) is a large part of its life.
+#ifndef OM_WF_LATE_GLOBAL
+#define OM_WF_LATE_GLOBAL 0
+#endif
+// Concurrent batches: stream 1's first batch starts once stream 0's first batch has launched
+// bounce OM_WF_STAGGER (0: at once), so one batch's light late bounces meet the other's heavy ones.
+#ifndef OM_WF_STAGGER
+#define OM_WF_STAGGER 0
+#endif
 constexpr uint32_t kTailSpbAsync = OM_WF_TAIL_SPB_ASYNC;
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
+// Merged late bounces (traced worlds): from bounce OM_WF_MERGE_AT on (0: never), a bounce
+// workgroup handles OM_WF_MERGE consecutive queue segments.  The late bounces carry few paths
+// per segment, yet each launch filled every CU with whole 512-lane workgroups (8 wave slots
+// each, mostly idle) that the other batch's heavy launches then lacked; merging divides those
+// launches' workgroups by OM_WF_MERGE.  Segment k's paths stay within merged segment k / F, so
+// nothing else changes (results are keyed by slot and (pixel, sample)).
+#ifndef OM_WF_MERGE_AT
+#define OM_WF_MERGE_AT 0
+#endif
+#ifndef OM_WF_MERGE
+#define OM_WF_MERGE 4
+#endif
+constexpr uint32_t kMergeMax = 16;
+static_assert(OM_WF_MERGE >= 1 && OM_WF_MERGE <= kMergeMax, "OM_WF_MERGE in [1, 16]");
 // Work distribution inside a bounce workgroup.  1 (default): every wave takes 64-path
 // chunks of the segment from an LDS counter and appends its survivors with one LDS atomic,
 // so the 8 waves never wait for each other; 0: the block walks the segment in 512-path
@@ -292,6 +332,12 @@ __device__ __forceinline__ void flush_counter(unsigned long long* ctr, int slot,
 struct Seg {
     uint32_t nseg;    // segments (= bounce workgroups)
     uint32_t segcap;  // paths per segment
+    // merged read (OM_WF_MERGE_AT, k_bounce b >= 1 only): workgroup s reads the input segments
+    // [s*fin, min((s+1)*fin, nseg_in)) of capacity segcap_in each and writes output segment s
+    // (capacity segcap = fin * segcap_in, so its survivors always fit); fin = 1: no merge
+    uint32_t fin = 1;
+    uint32_t segcap_in = 0;
+    uint32_t nseg_in = 0;
 };
 
 // One SoA path queue: o|depthf, d|first_id, throughput|segment, rng s|rng k|slot|-.
@@ -487,9 +533,23 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
                                                  const float2* __restrict__ hitbuf) {
     const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
     uint32_t n;
+    __shared__ uint32_t mpre[kMergeMax + 1];          // merged read: prefix of the input segments' counts
+    const bool merged = !FIRST && !HIT && G.fin > 1u;
     if (FIRST) {
         const uint64_t paths = (uint64_t)R.n_pixels * R.batch;
         n = seg0 < paths ? (uint32_t)std::min<uint64_t>(G.segcap, paths - seg0) : 0u;
+    } else if (merged) {
+        if (threadIdx.x == 0) {
+            uint32_t acc = 0;
+            for (uint32_t k = 0; k < G.fin; ++k) {
+                mpre[k] = acc;
+                const uint32_t si = blockIdx.x * G.fin + k;
+                acc += si < G.nseg_in ? count_in[si] : 0u;
+            }
+            mpre[G.fin] = acc;
+        }
+        __syncthreads();
+        n = mpre[G.fin];
     } else {
         n = count_in[blockIdx.x];
     }
@@ -519,7 +579,12 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR_B(FIRST) void k_bounce(OmSceneD
         Path p;
         uint32_t p_pixel = 0;
         if (jj < n) {
-            const uint64_t i = seg0 + jj;
+            uint64_t i = seg0 + jj;
+            if (merged) {                                 // input segment k of the workgroup's fin
+                uint32_t k = 0;
+                while (jj >= mpre[k + 1]) ++k;
+                i = (uint64_t)(blockIdx.x * G.fin + k) * G.segcap_in + (jj - mpre[k]);
+            }
             bool live = true;
             if (FIRST) {
                 live = gen_path(P, R, i, p, p_pixel, res_id);
@@ -867,6 +932,9 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmPar
 }
 
 // ---------------------------------------------------------------- accumulate
+#ifndef OM_ACC_GROUP
+#define OM_ACC_GROUP 8
+#endif
 template <bool COUNT>
 __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_stats* __restrict__ stats,
                                                      const uint32_t* __restrict__ pixels, uint32_t n_pixels, uint32_t by_pixel,
@@ -882,6 +950,37 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
         st.bloom = in.bloom; st.sx = in.sum[0]; st.sy = in.sum[1]; st.sz = in.sum[2]; st.n = in.n;
         st.avg_depth = in.avg_depth; st.bad = in.bad_avgs;
         st.rgbf = (uint32_t)in.color[0] | ((uint32_t)in.color[1] << 8) | ((uint32_t)in.color[2] << 16) | ((uint32_t)in.flags << 24);
+#if OM_ACC_GROUP > 1
+        // the loads of OM_ACC_GROUP samples are issued together (ids, then results and bloom
+        // words), then added in sample order: one lane's samples no longer cost a chain of
+        // dependent global round trips each (r03: 0.2-0.85 ms per 1080p x 16-spp launch before)
+        bool retired = false;
+        for (uint32_t s0 = 0; s0 < batch && !retired; s0 += OM_ACC_GROUP) {
+            const uint32_t m = batch - s0 < OM_ACC_GROUP ? batch - s0 : OM_ACC_GROUP;
+            uint32_t id[OM_ACC_GROUP];
+            float4 rr[OM_ACC_GROUP];
+            uint64_t bl[OM_ACC_GROUP];
+#pragma unroll
+            for (uint32_t j = 0; j < OM_ACC_GROUP; ++j) id[j] = j < m ? res_id[(uint64_t)(s0 + j) * n_pixels + k] : kNoSample;
+#pragma unroll
+            for (uint32_t j = 0; j < OM_ACC_GROUP; ++j) {
+                if (j < m) rr[j] = res[(uint64_t)(s0 + j) * n_pixels + k];
+                bl[j] = bloom[id[j] == kNoSample ? 0u : id[j]];
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < OM_ACC_GROUP; ++j) {                  // sample order == reference order
+                if (j >= m) break;
+                // adaptive batches of several samples: a pixel that retires at sample j takes no more
+                // (ThreadPixels::add_run, render_thread.rs:68-102); the batch's later samples of it
+                // were rendered speculatively and are dropped here
+                if (P.adaptive && (st.rgbf & 0x01000000u)) { retired = true; break; }
+                if (id[j] == kNoSample) continue;
+                const bool done = stats_add(st, f3(rr[j].x, rr[j].y, rr[j].z), rr[j].w, bl[j]);
+                if (COUNT) n_samples++;
+                credited += ((done && P.adaptive) ? (P.spp_total - st.n) : 0u) + 1u;   // render_thread.rs:196-198
+            }
+        }
+#else
         for (uint32_t s = 0; s < batch; ++s) {                                 // sample order == reference order
             // adaptive batches of several samples: a pixel that retires at sample j takes no more
             // (ThreadPixels::add_run, render_thread.rs:68-102); the batch's later samples of it
@@ -895,6 +994,7 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
             if (COUNT) n_samples++;
             credited += ((done && P.adaptive) ? (P.spp_total - st.n) : 0u) + 1u;   // render_thread.rs:196-198
         }
+#endif
         om_pixel_stats out;
         out.bloom = st.bloom; out.sum[0] = st.sx; out.sum[1] = st.sy; out.sum[2] = st.sz; out.n = st.n;
         out.avg_depth = st.avg_depth; out.bad_avgs = st.bad;
@@ -955,6 +1055,8 @@ Queue queue(QueueSet& B, int k) { return Queue{B.q[k][0], B.q[k][1], B.q[k][2], 
 struct Tail {
     hipStream_t st;
     hipEvent_t ev;
+    hipEvent_t stag = nullptr;   // recorded on the batch's stream after its bounce stag_at launch
+    uint32_t stag_at = 0;
 };
 template <int TR, bool COUNT, bool MARCH>
 __host__ inline void launch_tail(const Launch& L, QueueSet& B, Seg G, const Queue& in, const uint32_t* cin, uint32_t lds,
@@ -1030,9 +1132,10 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         return launches;
     }
     Tail TT = T;
+    const uint32_t cstride = G.nseg;                   // count arrays: one block of nseg per bounce
     for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
         const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
-        const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
+        const uint32_t* cin = B.counts + (size_t)bounce * cstride;
         if (bounce > 0 && bounce >= tail_at) {
             launch_tail<TR, COUNT, MARCH>(L, B, G, in, cin, lds, st, TT, tm, each);
             return launches + 1u;
@@ -1046,7 +1149,18 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
             st = TT.st;
             TT.ev = nullptr;
         }
-        uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
+        uint32_t* cout = B.counts + (size_t)(bounce + 1u) * cstride;
+        // merged late bounces: this launch reads F segments per workgroup and writes the merged
+        // geometry, which every later launch of the batch (and its tail) then uses
+        Seg GL = G;
+        if (OM_WF_MERGE_AT > 0 && OM_WF_MERGE > 1 && !OM_WF_DUAL && bounce == (uint32_t)OM_WF_MERGE_AT &&
+            G.nseg >= 2u * OM_WF_MERGE) {
+            // the last merged segment may take fewer input segments: its survivors still fit
+            // the queue, as they never outnumber its inputs
+            GL.nseg = (G.nseg + OM_WF_MERGE - 1u) / OM_WF_MERGE; GL.segcap = G.segcap * OM_WF_MERGE;
+            GL.fin = OM_WF_MERGE; GL.segcap_in = G.segcap; GL.nseg_in = G.nseg;
+            G.nseg = GL.nseg; G.segcap = GL.segcap;    // (k_tail takes any segment count)
+        }
         const int ti = each ? tm.begin(st) : -1;
         if (bounce == 0)
             hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, true>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
@@ -1056,10 +1170,15 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
             hipLaunchKernelGGL((k_bounce2<COUNT>), dim3(G.nseg), dim3(kBlk), lds + stack_bytes<TR_BVH2_LDS>(L.S), st, L.S,
                                L.P, G, in, cin, out, cout, B.res, B.res_id, L.counters);
 #endif
+        else if (OM_WF_LATE_GLOBAL > 0 && TR == TR_BVH2_LDS && bounce >= (uint32_t)OM_WF_LATE_GLOBAL)
+            hipLaunchKernelGGL((k_bounce<TR_BVH2_GLOBAL, COUNT, MARCH, false>), dim3(GL.nseg), dim3(kBlk),
+                               stack_bytes<TR_BVH2_GLOBAL>(L.S), st, L.S, L.P, GL, R, in, cin, out, cout, B.res, B.res_id,
+                               L.counters, (const float2*)nullptr);
         else
-            hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, R, in,
+            hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false>), dim3(GL.nseg), dim3(kBlk), lds, st, L.S, L.P, GL, R, in,
                                cin, out, cout, B.res, B.res_id, L.counters, (const float2*)nullptr);
         tm.end(ti, bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE, st);
+        if (T.stag && bounce == T.stag_at) (void)hipEventRecord(T.stag, st);
         ++launches;
     }
     if (TT.ev) { (void)hipEventRecord(TT.ev, st); (void)hipStreamWaitEvent(TT.st, TT.ev, 0); }
@@ -1169,8 +1288,13 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     // events: [0] call start on `st`, [k] side stream k joined (or, async tails: [1], [2] tail
     // streams done), [kMaxSets + i] batch i accumulated; async tails: [kMaxSets + nb + i] batch
     // i's bounces launched (its tail waits on it)
+    // accumulate stream: events [kMaxSets + i] batch i accumulated (as before), [kMaxSets + nb + i]
+    // batch i rendered, [kMaxSets + 2nb] the stagger point, [kMaxSets + 2nb + 1] the accumulate
+    // stream's end of call
+    const bool acc_stream = OM_WF_ACC_STREAM && concurrent && ns >= 2u && !async_tail;
+    const size_t ev_stag = kMaxSets + 2u * (size_t)nb, ev_accend = ev_stag + 1u;
     if (ns > 1) {
-        if ((e = ensure_events(B, kMaxSets + 2u * nb)) != hipSuccess) { err = "event creation failed"; return e; }
+        if ((e = ensure_events(B, kMaxSets + 2u * nb + 2u)) != hipSuccess) { err = "event creation failed"; return e; }
         (void)hipEventRecord(B.ev[0], st);                       // side streams start after everything before the call
         for (uint32_t k = 1; k < ns; ++k) {
             if (!B.side[k] && (e = hipStreamCreateWithFlags(&B.side[k], hipStreamNonBlocking)) != hipSuccess) {
@@ -1193,15 +1317,48 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
             (void)hipStreamWaitEvent(B.tail[k], B.ev[0], 0);
         }
     }
+    if (acc_stream) {
+        if (!B.acc && (e = hipStreamCreateWithFlags(&B.acc, hipStreamNonBlocking)) != hipSuccess) {
+            err = "accumulate stream creation failed"; return e;
+        }
+        bool have = B.alt_cap >= B.cap;
+        for (uint32_t k = 0; k < ns; ++k) have = have && B.alt_res[k] && B.alt_id[k];
+        if (!have) {
+            for (int k = 0; k < kMaxSets; ++k) {
+                if (B.alt_res[k]) (void)hipFree(B.alt_res[k]);
+                if (B.alt_id[k]) (void)hipFree(B.alt_id[k]);
+                B.alt_res[k] = nullptr; B.alt_id[k] = nullptr;
+            }
+            B.alt_cap = 0;
+            for (uint32_t k = 0; k < ns; ++k) {
+                if ((e = hipMalloc(&B.alt_res[k], B.cap * sizeof(float4))) != hipSuccess ||
+                    (e = hipMalloc(&B.alt_id[k], B.cap * sizeof(uint32_t))) != hipSuccess) {
+                    err = "result buffer allocation failed"; return e;
+                }
+            }
+            B.alt_cap = B.cap;
+        }
+        (void)hipStreamWaitEvent(B.acc, B.ev[0], 0);
+    }
     uint32_t launches = 0;
     for (uint32_t i = 0, done = 0; i < nb; ++i) {
         const uint32_t b = std::min(batch, L.P.sample_count - done);
         const uint64_t paths = (uint64_t)n_px * b;
         hipStream_t si = streams[i % ns];
-        QueueSet& QS = B.set[i % nsets];
+        // accumulate stream: odd rounds of a stream write the set's second result buffer, and a
+        // result buffer is rewritten only once the batch that last wrote it is accumulated
+        QueueSet QS = B.set[i % nsets];                          // (a shallow copy: pointers only)
+        if (acc_stream) {
+            if ((i / ns) & 1u) { QS.res = B.alt_res[i % ns]; QS.res_id = B.alt_id[i % ns]; }
+            if (i >= 2u * ns) (void)hipStreamWaitEvent(si, B.ev[kMaxSets + i - 2u * ns], 0);
+        }
         // async tails: batch i's tail + accumulate go on tail stream i % 2, behind its bounces; the
         // queue set is reused by batch i + nsets only after batch i is accumulated
-        const Tail TT{async_tail ? B.tail[i % 2u] : si, async_tail ? B.ev[kMaxSets + nb + i] : nullptr};
+        Tail TT{async_tail ? B.tail[i % 2u] : si, async_tail ? B.ev[kMaxSets + nb + i] : nullptr};
+        if (OM_WF_STAGGER > 0 && ns > 1) {
+            if (i == 0) { TT.stag = B.ev[ev_stag]; TT.stag_at = OM_WF_STAGGER; }
+            if (i == 1) (void)hipStreamWaitEvent(si, B.ev[ev_stag], 0);
+        }
         if (async_tail && i >= nsets) (void)hipStreamWaitEvent(si, B.ev[kMaxSets + i - nsets], 0);
         Seg G;
         G.nseg = nseg;
@@ -1218,8 +1375,14 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
             case TR_BVH4_GLOBAL: launches += run_tr<TR_BVH4_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
             default: launches += run_tr<TR_BVH2_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds, TT); break;
         }
-        if (async_tail) si = TT.st;                                  // accumulate behind the tail
-        if (ns > 1 && i > 0) (void)hipStreamWaitEvent(si, B.ev[kMaxSets + i - 1u], 0);   // Stats::add in sample order
+        if (acc_stream) {                                            // accumulate stream: in order by itself
+            (void)hipEventRecord(B.ev[kMaxSets + nb + i], si);
+            (void)hipStreamWaitEvent(B.acc, B.ev[kMaxSets + nb + i], 0);
+            si = B.acc;
+        } else {
+            if (async_tail) si = TT.st;                              // accumulate behind the tail
+            if (ns > 1 && i > 0) (void)hipStreamWaitEvent(si, B.ev[kMaxSets + i - 1u], 0);   // Stats::add in sample order
+        }
         const uint32_t grid_a = (n_px + kBlk - 1) / kBlk;
         const int ati = tm.mode == 1 ? tm.begin(si) : -1;
         if (L.count)
@@ -1252,6 +1415,10 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
         for (uint32_t k = 1; k < ns; ++k) {
             (void)hipEventRecord(B.ev[k], streams[k]);
             (void)hipStreamWaitEvent(st, B.ev[k], 0);
+        }
+        if (acc_stream) {
+            (void)hipEventRecord(B.ev[ev_accend], B.acc);
+            (void)hipStreamWaitEvent(st, B.ev[ev_accend], 0);
         }
     }
     tm.end(call_ti, OM_KT_BOUNCE_SPAN, st, launches);

@@ -130,6 +130,25 @@ declare -A V=(
   [first7b]="$COMMON $DEV -DOM_WF_WAVES_FIRST=7"
   [dual6]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=6 -DOM_B2_DIRECT=0"
   [dual5]="$COMMON $DEV -DOM_WF_DUAL=1 -DOM_WF_DUAL_WAVES=5 -DOM_B2_DIRECT=0"
+  # r03: merged late bounces (from bounce M, F segments per workgroup) and grouped accumulate loads
+  [m6f4]="$COMMON $DEV -DOM_WF_MERGE_AT=6 -DOM_WF_MERGE=4"
+  [m8f4]="$COMMON $DEV -DOM_WF_MERGE_AT=8 -DOM_WF_MERGE=4"
+  [m6f8]="$COMMON $DEV -DOM_WF_MERGE_AT=6 -DOM_WF_MERGE=8"
+  [m10f8]="$COMMON $DEV -DOM_WF_MERGE_AT=10 -DOM_WF_MERGE=8"
+  [acc8]="$COMMON $DEV -DOM_ACC_GROUP=8"
+  [acc1]="$COMMON $DEV -DOM_ACC_GROUP=1"
+  [acc8m8f4]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_MERGE_AT=8 -DOM_WF_MERGE=4"
+  # r03: accumulates on their own stream (no lockstep through the accumulate chain), with and
+  # without a stagger of stream 1's first batch, with merged late bounces
+  [as]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_ACC_STREAM=1"
+  [asm]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_ACC_STREAM=1 -DOM_WF_MERGE_AT=8 -DOM_WF_MERGE=4"
+  [asmst4]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_ACC_STREAM=1 -DOM_WF_MERGE_AT=8 -DOM_WF_MERGE=4 -DOM_WF_STAGGER=4"
+  [asst4]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_ACC_STREAM=1 -DOM_WF_STAGGER=4"
+  [asst2]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_ACC_STREAM=1 -DOM_WF_STAGGER=2"
+  # r03: late bounces read the BVH2 through the caches (no LDS staging) from bounce K
+  [lg6]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_LATE_GLOBAL=6"
+  [lg9]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_LATE_GLOBAL=9"
+  [lg12]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_LATE_GLOBAL=12"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
