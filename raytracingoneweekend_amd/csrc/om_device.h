@@ -215,7 +215,30 @@ __device__ __forceinline__ bool bary_root(const OmBary& B, F3 o, F3 d, float tmi
 }
 
 // ---------------------------------------------------------------- marched.rs
-__device__ __forceinline__ float len3(F3 a) { return sqrtf(dot(a, a)); }
+// Square roots of the march SDFs.  hipcc's correctly rounded f32 sqrt is v_sqrt_f32 (<= 1 ulp)
+// plus a +-1-ulp correction, wrapped in range handling: inputs below 2^-96 are scaled by 2^32
+// (and the root by 2^-16), and +-0 / +inf pass through a class test.  For x >= 2^-96 (and
+// +inf) the wrapper selects nothing, so when every lane of the wave is in that range
+// (OM_MARCH_SQRT_CORE) the core alone runs: the same v_sqrt_f32, the same two fma residuals
+// and selects, hence the same bits, and ~7 fewer VALU (+2 s_nop) per root.  Otherwise the
+// whole wave takes sqrtf.  NaN inputs (never in range) always take sqrtf.
+#ifndef OM_MARCH_SQRT_CORE
+#define OM_MARCH_SQRT_CORE 0
+#endif
+__device__ __forceinline__ float sqrt_cr_core(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
+    r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
+    return r;
+}
+__device__ __forceinline__ float march_sqrt(float x) {
+#if OM_MARCH_SQRT_CORE
+    if (__ballot(!(x >= 0x1p-96f)) == 0) return sqrt_cr_core(x);
+#endif
+    return sqrtf(x);
+}
+__device__ __forceinline__ float len3(F3 a) { return march_sqrt(dot(a, a)); }
 // MarchedSphere (marched.rs:56-76): to_local = p - w*center (w = 1)
 __device__ __forceinline__ float msphere_sdf(const OmMSphere& S, F3 p) {
     const F3 c = ld3(S.center);
@@ -235,8 +258,8 @@ __device__ __forceinline__ float mbox_sdf(const OmMBox& B, F3 p) { return mbox_l
 // MarchedTorus (marched.rs:133-151); TT = OmMTorus or the march's SDF-only copy (om_trace.h)
 template <class TT>
 __device__ __forceinline__ float mtorus_local(const TT& T, F3 p) {
-    const float qx = sqrtf((p.x * p.x + p.z * p.z) + 0.0f * 0.0f) - T.sizes[0];
-    return sqrtf((qx * qx + p.y * p.y) + 0.0f * 0.0f) - T.sizes[1];
+    const float qx = march_sqrt((p.x * p.x + p.z * p.z) + 0.0f * 0.0f) - T.sizes[0];
+    return march_sqrt((qx * qx + p.y * p.y) + 0.0f * 0.0f) - T.sizes[1];
 }
 template <class TT>
 __device__ __forceinline__ F3 mtorus_to_local(const TT& T, F3 p) {

@@ -149,6 +149,8 @@ declare -A V=(
   [lg6]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_LATE_GLOBAL=6"
   [lg9]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_LATE_GLOBAL=9"
   [lg12]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_LATE_GLOBAL=12"
+  # r03: march SDF roots as hipcc's sqrt core when the whole wave is in range (same bits)
+  [sqcore]="$COMMON $DEV -DOM_MARCH_SQRT_CORE=1"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
