@@ -367,22 +367,54 @@ struct Path {
     Rng g;
 };
 
+// OM_WF_NT_LOADS: the path-state loads carry the non-temporal hint (each 16-B lane record is read
+// once per bounce), so the streaming queues do not evict the leaf records and nodes the trace
+// re-reads from the vector L1.  Component loads keep the scalar register shapes (a native
+// 4-vector load moved k_bounce into scratch spills in r01); the compiler still merges them into
+// global_load_dwordx4 ... nt.  C1 with both hints: 7096 / 7114 vs 7094 / 7068 Msamples/s (r03_v13).
+#ifndef OM_WF_NT_LOADS
+#define OM_WF_NT_LOADS 1
+#endif
+template <class V>
+__device__ __forceinline__ V ld4(const V* q) {
+#if OM_WF_NT_LOADS
+    V v;
+    v.x = __builtin_nontemporal_load(&q->x); v.y = __builtin_nontemporal_load(&q->y);
+    v.z = __builtin_nontemporal_load(&q->z); v.w = __builtin_nontemporal_load(&q->w);
+    return v;
+#else
+    return *q;
+#endif
+}
 __device__ __forceinline__ void load_ray(const Queue& Q, uint64_t i, Path& p) {
-    const float4 a = Q.q0[i], b = Q.q1[i];
+    const float4 a = ld4(Q.q0 + i), b = ld4(Q.q1 + i);
     p.o = f3(a.x, a.y, a.z); p.depthf = a.w;
     p.d = f3(b.x, b.y, b.z); p.first_id = __float_as_uint(b.w);
 }
 __device__ __forceinline__ void load_rest(const Queue& Q, uint64_t i, Path& p) {
-    const float4 c = Q.q2[i];
-    const uint4 r = Q.qr[i];
+    const float4 c = ld4(Q.q2 + i);
+    const uint4 r = ld4(Q.qr + i);
     p.cur = f3(c.x, c.y, c.z); p.seg = __float_as_uint(c.w);
     p.g.s = r.x; p.g.k = r.y; p.slot = r.z;
 }
+// OM_WF_NT_STORES: the same hint on the path-state stores (read back only by the next launch).
+#ifndef OM_WF_NT_STORES
+#define OM_WF_NT_STORES 1
+#endif
+template <class V>
+__device__ __forceinline__ void st4(V* q, V v) {
+#if OM_WF_NT_STORES
+    __builtin_nontemporal_store(v.x, &q->x); __builtin_nontemporal_store(v.y, &q->y);
+    __builtin_nontemporal_store(v.z, &q->z); __builtin_nontemporal_store(v.w, &q->w);
+#else
+    *q = v;
+#endif
+}
 __device__ __forceinline__ void store_path(const Queue& Q, uint64_t i, const Path& p) {
-    Q.q0[i] = make_float4(p.o.x, p.o.y, p.o.z, p.depthf);
-    Q.q1[i] = make_float4(p.d.x, p.d.y, p.d.z, __uint_as_float(p.first_id));
-    Q.q2[i] = make_float4(p.cur.x, p.cur.y, p.cur.z, __uint_as_float(p.seg));
-    Q.qr[i] = make_uint4(p.g.s, p.g.k, p.slot, 0u);
+    st4(Q.q0 + i, make_float4(p.o.x, p.o.y, p.o.z, p.depthf));
+    st4(Q.q1 + i, make_float4(p.d.x, p.d.y, p.d.z, __uint_as_float(p.first_id)));
+    st4(Q.q2 + i, make_float4(p.cur.x, p.cur.y, p.cur.z, __uint_as_float(p.seg)));
+    st4(Q.qr + i, make_uint4(p.g.s, p.g.k, p.slot, 0u));
 }
 
 // Scene data a workgroup traces against: BVH2/BVH4 nodes + leaf table staged in LDS behind

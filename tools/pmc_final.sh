@@ -1,0 +1,23 @@
+#!/bin/bash
+# End-of-round PMC passes (GPU box), summarised on the box so gpurun_out/ stays small:
+#   C1 all five passes -> pmc_summary_C1.json + pmc_traffic.json; C2 all five -> *_C2.json;
+#   C4 the FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic_C4.json.  Raw pass files are deleted.
+#   bash tools/pmc_final.sh TAG      -> gpurun_out/TAG/pmc_*.json
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+TAG=${1:-pmc_final}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+run() {   # name, passes, bench args...
+  local name=$1 passes=$2; shift 2
+  PASSES="$passes" bash tools/pmc.sh "$TAG/raw_$name" "$@" > "$OUT/pmc_$name.log" 2>&1 || { echo "pmc $name failed"; return 1; }
+  if [ "$passes" != "3 4" ]; then
+    python tools/pmc_summary.py "$OUT/raw_$name" > "$OUT/pmc_summary_$name.json" || return 1
+  fi
+  python tools/pmc_traffic.py "$OUT/raw_$name" "$OUT/pmc_traffic_$name.json" || return 1
+  rm -rf "$OUT/raw_$name"
+}
+run C1 "1 2 3 4 5" --no-extras || exit 1
+run C2 "1 2 3 4 5" --config C2 --no-extras || exit 1
+run C4 "3 4" --config C4 --no-extras || exit 1
+echo ok
