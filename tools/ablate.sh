@@ -156,6 +156,8 @@ declare -A V=(
   [nt0]="$COMMON $DEV -DOM_WF_NT_LOADS=0 -DOM_WF_NT_STORES=0"
   [nts]="$COMMON $DEV -DOM_WF_NT_LOADS=0 -DOM_WF_NT_STORES=1"
   [ntls]="$COMMON $DEV -DOM_WF_NT_LOADS=1 -DOM_WF_NT_STORES=1"
+  # r03: 32-spp batches (2^26 paths at 1080p) instead of 16
+  [bs32]="$COMMON $DEV -DOM_WF_BATCH_SPP=32"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
