@@ -177,6 +177,9 @@ static_assert(OM_WF_MERGE >= 1 && OM_WF_MERGE <= kMergeMax, "OM_WF_MERGE in [1, 
 #ifndef OM_WF_BATCH_SPP
 #define OM_WF_BATCH_SPP 16
 #endif
+#ifndef OM_WF_MIN_PATHS_LOG2
+#define OM_WF_MIN_PATHS_LOG2 25
+#endif
 // Bounce 0 with primary tile lists: a wave whose lanes all lie in one 8x8 tile (every wave but
 // those where partial tiles meet) reads the tile's list and records with scalar loads.
 #ifndef OM_TILES_UNIFORM
@@ -1264,7 +1267,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     // like 1080p instead of 4-spp ones, whose 4x launches and 4x Stats read-modify-write per sample
     // cost C4 ~11% in k_accumulate alone (r03)
     const uint64_t kMaxPaths = std::min<uint64_t>(1ull << OM_WF_MAX_PATHS_LOG2,
-                                                  std::max<uint64_t>(1ull << 25, (uint64_t)OM_WF_BATCH_SPP * n_px));
+                                                  std::max<uint64_t>(1ull << OM_WF_MIN_PATHS_LOG2, (uint64_t)OM_WF_BATCH_SPP * n_px));
     const uint32_t want = std::max<uint32_t>(1u, std::min<uint32_t>(L.streams, (uint32_t)kMaxSets));
     const bool concurrent = !L.P.adaptive && want >= 2u && L.P.sample_count >= 2u;
     uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));

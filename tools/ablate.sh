@@ -158,6 +158,8 @@ declare -A V=(
   [ntls]="$COMMON $DEV -DOM_WF_NT_LOADS=1 -DOM_WF_NT_STORES=1"
   # r03: 32-spp batches (2^26 paths at 1080p) instead of 16
   [bs32]="$COMMON $DEV -DOM_WF_BATCH_SPP=32"
+  [bs8]="$COMMON $DEV -DOM_WF_BATCH_SPP=8 -DOM_WF_MIN_PATHS_LOG2=20"
+  [bs12]="$COMMON $DEV -DOM_WF_BATCH_SPP=12 -DOM_WF_MIN_PATHS_LOG2=20"
 )
 if [ "$1" = list ]; then echo "${!V[@]}"; exit 0; fi
 if [ "$1" = resources ]; then
