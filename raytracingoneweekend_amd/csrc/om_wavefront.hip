@@ -227,6 +227,10 @@ __host__ __device__ constexpr bool exact_view_built() { return OM_WF_MARCH_EXACT
 #ifndef OM_WF_REFILL
 #define OM_WF_REFILL 16
 #endif
+// k_march: march steps per refill check (the check costs three ballots and its branches)
+#ifndef OM_MARCH_UNROLL
+#define OM_MARCH_UNROLL 1
+#endif
 // Adaptive calls: samples per pixel per (serial) batch.  Bounce 0 reads each pixel's retirement
 // flag at the batch start; a pixel that retires inside a batch has its remaining samples of
 // that batch rendered and dropped by k_accumulate (the result is the sequential one).  C1
@@ -862,13 +866,16 @@ __device__ __forceinline__ void march_lanes(const OmSceneDev& S, const OmParamsD
     if (act) start();
     PH_WAIT_LAP(0);
     for (;;) {
-        if (act) {
-            int gi = -1;
-            const int r = marching ? march_step(S, m, o, d, P.tmax, closest, t, iters, gi, w) : 2;
-            if (r != 0) {
-                if (r == 1) { best = gi; closest = t; }
-                hit[seg0 + j] = make_float2(closest, __int_as_float(best));
-                act = false;
+#pragma unroll
+        for (int u = 0; u < OM_MARCH_UNROLL; ++u) {     // march steps between refill checks
+            if (act) {
+                int gi = -1;
+                const int r = marching ? march_step(S, m, o, d, P.tmax, closest, t, iters, gi, w) : 2;
+                if (r != 0) {
+                    if (r == 1) { best = gi; closest = t; }
+                    hit[seg0 + j] = make_float2(closest, __int_as_float(best));
+                    act = false;
+                }
             }
         }
         PH_WAIT_LAP(1);

@@ -3,7 +3,7 @@
 # _abl/; build them first with `VARIANTS="..." bash tools/ablate.sh build`).  Each run checks the
 # candidate build's parity through OM_LIB where it changes code, then alternates the variants.
 #   bash tools/ab_r03.sh EXPERIMENT [TAG]      -> gpurun_out/TAG/...
-# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2
+# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -59,6 +59,12 @@ case $EXP in
   batch2)       # 8- and 12-spp batches
     bash tools/ab.sh "$TAG/ab_bs8_128" "base bs8 bs8 base" || exit 1
     bash tools/ab.sh "$TAG/ab_bs12_96" "base bs12 bs12 base" --spp-per-step 96 --steps 6 || exit 1 ;;
+  munroll)      # k_march steps per refill check (C2)
+    parity mu2 $P || exit 1
+    bash tools/ab.sh "$TAG/ab_munroll_C2" "base mu2 mu4 mu2r8 mu2r8 mu4 mu2 base" --config C2 || exit 1 ;;
+  munroll2)     # more steps per check, refill thresholds (C2)
+    parity mu8 $P || exit 1
+    bash tools/ab.sh "$TAG/ab_munroll2_C2" "mu4 mu6 mu8 mu4r24 mu4r32 mu8r32 mu8r32 mu4r32 mu4r24 mu8 mu6 mu4" --config C2 || exit 1 ;;
   *) echo "unknown experiment $EXP"; exit 2 ;;
 esac
 echo ok

@@ -158,6 +158,15 @@ declare -A V=(
   [ntls]="$COMMON $DEV -DOM_WF_NT_LOADS=1 -DOM_WF_NT_STORES=1"
   # r03: 32-spp batches (2^26 paths at 1080p) instead of 16
   [bs32]="$COMMON $DEV -DOM_WF_BATCH_SPP=32"
+  # r03: k_march steps per refill check
+  [mu2]="$COMMON $DEV -DOM_MARCH_UNROLL=2"
+  [mu4]="$COMMON $DEV -DOM_MARCH_UNROLL=4"
+  [mu2r8]="$COMMON $DEV -DOM_MARCH_UNROLL=2 -DOM_WF_REFILL=8"
+  [mu8]="$COMMON $DEV -DOM_MARCH_UNROLL=8"
+  [mu6]="$COMMON $DEV -DOM_MARCH_UNROLL=6"
+  [mu4r24]="$COMMON $DEV -DOM_MARCH_UNROLL=4 -DOM_WF_REFILL=24"
+  [mu4r32]="$COMMON $DEV -DOM_MARCH_UNROLL=4 -DOM_WF_REFILL=32"
+  [mu8r32]="$COMMON $DEV -DOM_MARCH_UNROLL=8 -DOM_WF_REFILL=32"
   [bs8]="$COMMON $DEV -DOM_WF_BATCH_SPP=8 -DOM_WF_MIN_PATHS_LOG2=20"
   [bs12]="$COMMON $DEV -DOM_WF_BATCH_SPP=12 -DOM_WF_MIN_PATHS_LOG2=20"
 )
