@@ -167,6 +167,10 @@ declare -A V=(
   [mu4r24]="$COMMON $DEV -DOM_MARCH_UNROLL=4 -DOM_WF_REFILL=24"
   [mu4r32]="$COMMON $DEV -DOM_MARCH_UNROLL=4 -DOM_WF_REFILL=32"
   [mu8r32]="$COMMON $DEV -DOM_MARCH_UNROLL=8 -DOM_WF_REFILL=32"
+  [mu1]="$COMMON $DEV -DOM_MARCH_UNROLL=1"
+  [mu12]="$COMMON $DEV -DOM_MARCH_UNROLL=12"
+  [mu16]="$COMMON $DEV -DOM_MARCH_UNROLL=16"
+  [mu8r12]="$COMMON $DEV -DOM_MARCH_UNROLL=8 -DOM_WF_REFILL=12"
   [bs8]="$COMMON $DEV -DOM_WF_BATCH_SPP=8 -DOM_WF_MIN_PATHS_LOG2=20"
   [bs12]="$COMMON $DEV -DOM_WF_BATCH_SPP=12 -DOM_WF_MIN_PATHS_LOG2=20"
 )
