@@ -16,6 +16,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --outpu
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --kernel-timing launch > "$OUT/bench_launch_timing.json" 2>> "$OUT/bench.err" || { echo "bench (launch timing) failed"; exit 1; }
 timeout -k 10 300 python bench.py --no-cpu-baseline --no-extras --kernel-timing off > "$OUT/bench_notiming.json" 2>> "$OUT/bench.err" || { echo "bench (no timing) failed"; exit 1; }
 if [ -z "$NO_PMC" ]; then
-  bash tools/pmc.sh "$TAG/pmc" --no-extras > "$OUT/pmc.log" 2>&1 || { echo "pmc failed"; exit 1; }
+  CONFIGS=C1 bash tools/pmc_final.sh "$TAG/pmc" > "$OUT/pmc.log" 2>&1 || { echo "pmc failed"; exit 1; }
 fi
 echo ok
