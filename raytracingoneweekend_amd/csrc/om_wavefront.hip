@@ -925,6 +925,9 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_march(OmSceneDev S, OmPa
 }
 
 // ---------------------------------------------------------------- tail
+#ifndef OM_WF_TAIL_SETPRIO
+#define OM_WF_TAIL_SETPRIO 0
+#endif
 // Workgroup b: every path of segments [b*kTailSpb, (b+1)*kTailSpb) of queue `in`, each
 // run to completion; a lane whose path ends takes the next one from an LDS counter.
 template <int TR, bool COUNT, bool MARCH, uint32_t SPB = kTailSpb>
@@ -946,6 +949,9 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmPar
     __syncthreads();
     const uint32_t total = pre[SPB];
     if (total == 0) return;
+    // the tail is a few long chains beside the other stream's full launches: a raised wave
+    // priority lets its waves issue first on the SIMDs they share (OM_WF_TAIL_SETPRIO, 0 = off)
+    if (OM_WF_TAIL_SETPRIO > 0) __builtin_amdgcn_s_setprio(OM_WF_TAIL_SETPRIO);
     const Tracer T = stage_scene<TR>(S);
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
     WorkT<COUNT> w;
@@ -979,6 +985,9 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmPar
 }
 
 // ---------------------------------------------------------------- accumulate
+#ifndef OM_ACC_SETPRIO
+#define OM_ACC_SETPRIO 0
+#endif
 #ifndef OM_ACC_GROUP
 #define OM_ACC_GROUP 8
 #endif
@@ -988,6 +997,7 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
                                                      uint32_t batch, const float4* __restrict__ res,
                                                      const uint32_t* __restrict__ res_id, const uint64_t* __restrict__ bloom,
                                                      unsigned long long* __restrict__ counters) {
+    if (OM_ACC_SETPRIO > 0) __builtin_amdgcn_s_setprio(OM_ACC_SETPRIO);
     const uint32_t k = blockIdx.x * kBlk + threadIdx.x;
     uint32_t n_samples = 0, credited = 0;
     if (k < n_pixels) {

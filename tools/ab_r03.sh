@@ -3,7 +3,7 @@
 # _abl/; build them first with `VARIANTS="..." bash tools/ablate.sh build`).  Each run checks the
 # candidate build's parity through OM_LIB where it changes code, then alternates the variants.
 #   bash tools/ab_r03.sh EXPERIMENT [TAG]      -> gpurun_out/TAG/...
-# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3
+# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -67,6 +67,9 @@ case $EXP in
     bash tools/ab.sh "$TAG/ab_munroll2_C2" "mu4 mu6 mu8 mu4r24 mu4r32 mu8r32 mu8r32 mu4r32 mu4r24 mu8 mu6 mu4" --config C2 || exit 1 ;;
   munroll3)     # around the default (8 steps per check)
     bash tools/ab.sh "$TAG/ab_munroll3_C2" "base mu12 mu16 mu8r12 mu8r12 mu16 mu12 base" --config C2 || exit 1 ;;
+  setprio)      # raised wave priority for the tail / accumulate (C1, then C2)
+    bash tools/ab.sh "$TAG/ab_setprio_C1" "base tp2 tp3 tpa2 tpa2 tp3 tp2 base" || exit 1
+    bash tools/ab.sh "$TAG/ab_setprio_C2" "base tp2 tp2 base" --config C2 || exit 1 ;;
   *) echo "unknown experiment $EXP"; exit 2 ;;
 esac
 echo ok

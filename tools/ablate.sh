@@ -168,6 +168,10 @@ declare -A V=(
   [mu4r32]="$COMMON $DEV -DOM_MARCH_UNROLL=4 -DOM_WF_REFILL=32"
   [mu8r32]="$COMMON $DEV -DOM_MARCH_UNROLL=8 -DOM_WF_REFILL=32"
   [mu1]="$COMMON $DEV -DOM_MARCH_UNROLL=1"
+  # r03: raised wave priority for the tail / the accumulate (s_setprio)
+  [tp2]="$COMMON $DEV -DOM_WF_TAIL_SETPRIO=2"
+  [tp3]="$COMMON $DEV -DOM_WF_TAIL_SETPRIO=3"
+  [tpa2]="$COMMON $DEV -DOM_WF_TAIL_SETPRIO=2 -DOM_ACC_SETPRIO=2"
   [mu12]="$COMMON $DEV -DOM_MARCH_UNROLL=12"
   [mu16]="$COMMON $DEV -DOM_MARCH_UNROLL=16"
   [mu8r12]="$COMMON $DEV -DOM_MARCH_UNROLL=8 -DOM_WF_REFILL=12"
