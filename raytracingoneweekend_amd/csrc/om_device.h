@@ -22,8 +22,37 @@ __device__ __forceinline__ F3 mul(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, 
 __device__ __forceinline__ F3 scl(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }       // vec3.rs:220-235
 __device__ __forceinline__ F3 neg(F3 a) { return f3(-a.x, -a.y, -a.z); }
 __device__ __forceinline__ float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }    // vec3.rs:29-31
+// Square roots of the march SDFs.  hipcc's correctly rounded f32 sqrt is v_sqrt_f32 (<= 1 ulp)
+// plus a +-1-ulp correction, wrapped in range handling: inputs below 2^-96 are scaled by 2^32
+// (and the root by 2^-16), and +-0 / +inf pass through a class test.  For x >= 2^-96 (and
+// +inf) the wrapper selects nothing, so when every lane of the wave is in that range
+// (OM_MARCH_SQRT_CORE) the core alone runs: the same v_sqrt_f32, the same two fma residuals
+// and selects, hence the same bits, and ~7 fewer VALU (+2 s_nop) per root.  Otherwise the
+// whole wave takes sqrtf.  NaN inputs (never in range) always take sqrtf.
+#ifndef OM_MARCH_SQRT_CORE
+#define OM_MARCH_SQRT_CORE 0
+#endif
+__device__ __forceinline__ float sqrt_cr_core(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
+    r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
+    return r;
+}
+template <bool CORE>
+__device__ __forceinline__ float sqrt_w(float x) {
+    if constexpr (CORE) {
+        if (__ballot(!(x >= 0x1p-96f)) == 0) return sqrt_cr_core(x);
+    }
+    return sqrtf(x);
+}
+__device__ __forceinline__ float march_sqrt(float x) { return sqrt_w<OM_MARCH_SQRT_CORE != 0>(x); }
+// OM_SQRT_CORE: the same for unit() and the sphere tests' discriminant roots (measured, off)
+#ifndef OM_SQRT_CORE
+#define OM_SQRT_CORE 0
+#endif
 __device__ __forceinline__ F3 unit(F3 a) {                                                        // vec3.rs:35-40, 236-240
-    const float len = sqrtf(dot(a, a));
+    const float len = sqrt_w<OM_SQRT_CORE != 0>(dot(a, a));
     return scl(a, 1.0f / len);
 }
 __device__ __forceinline__ F3 at(F3 o, F3 d, float t) { return add(o, scl(d, t)); }              // ray.rs:14-16 (t*dir == dir*t)
@@ -89,7 +118,7 @@ __device__ __forceinline__ bool sphere_root_local(F3 lo, F3 ld, float tmin, floa
     const float c = dot(lo, lo) - 1.0f;
     const float disc = half_b * half_b - a * c;
     if (disc < 0.0f) return false;
-    const float sqrtd = sqrtf(disc);
+    const float sqrtd = sqrt_w<OM_SQRT_CORE != 0>(disc);
     const float n1 = -half_b - sqrtd, n2 = -half_b + sqrtd;
     if (OM_SPHERE_FAST_REJECT || FASTREJ) {
     // Both roots provably outside [tmin, tmax] without the two correctly rounded divisions
@@ -130,7 +159,7 @@ __device__ __forceinline__ SpherePre sphere_pre(const OmAffineTest& T, F3 o, F3 
     const float disc = half_b * half_b - a * c;
     SpherePre p;
     p.ok = !(disc < 0.0f);
-    const float sqrtd = sqrtf(disc);
+    const float sqrtd = sqrt_w<OM_SQRT_CORE != 0>(disc);
     p.r1 = (-half_b - sqrtd) / a;
     p.r2 = (-half_b + sqrtd) / a;
     return p;
@@ -215,29 +244,6 @@ __device__ __forceinline__ bool bary_root(const OmBary& B, F3 o, F3 d, float tmi
 }
 
 // ---------------------------------------------------------------- marched.rs
-// Square roots of the march SDFs.  hipcc's correctly rounded f32 sqrt is v_sqrt_f32 (<= 1 ulp)
-// plus a +-1-ulp correction, wrapped in range handling: inputs below 2^-96 are scaled by 2^32
-// (and the root by 2^-16), and +-0 / +inf pass through a class test.  For x >= 2^-96 (and
-// +inf) the wrapper selects nothing, so when every lane of the wave is in that range
-// (OM_MARCH_SQRT_CORE) the core alone runs: the same v_sqrt_f32, the same two fma residuals
-// and selects, hence the same bits, and ~7 fewer VALU (+2 s_nop) per root.  Otherwise the
-// whole wave takes sqrtf.  NaN inputs (never in range) always take sqrtf.
-#ifndef OM_MARCH_SQRT_CORE
-#define OM_MARCH_SQRT_CORE 0
-#endif
-__device__ __forceinline__ float sqrt_cr_core(float x) {
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
-    float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
-    r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
-    return r;
-}
-__device__ __forceinline__ float march_sqrt(float x) {
-#if OM_MARCH_SQRT_CORE
-    if (__ballot(!(x >= 0x1p-96f)) == 0) return sqrt_cr_core(x);
-#endif
-    return sqrtf(x);
-}
 __device__ __forceinline__ float len3(F3 a) { return march_sqrt(dot(a, a)); }
 // MarchedSphere (marched.rs:56-76): to_local = p - w*center (w = 1)
 __device__ __forceinline__ float msphere_sdf(const OmMSphere& S, F3 p) {

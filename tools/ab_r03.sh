@@ -3,7 +3,7 @@
 # _abl/; build them first with `VARIANTS="..." bash tools/ablate.sh build`).  Each run checks the
 # candidate build's parity through OM_LIB where it changes code, then alternates the variants.
 #   bash tools/ab_r03.sh EXPERIMENT [TAG]      -> gpurun_out/TAG/...
-# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio
+# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio | sqall
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -70,6 +70,10 @@ case $EXP in
   setprio)      # raised wave priority for the tail / accumulate (C1, then C2)
     bash tools/ab.sh "$TAG/ab_setprio_C1" "base tp2 tp3 tpa2 tpa2 tp3 tp2 base" || exit 1
     bash tools/ab.sh "$TAG/ab_setprio_C2" "base tp2 tp2 base" --config C2 || exit 1 ;;
+  sqall)        # the bare sqrt core in unit() and the sphere tests (C1, C3)
+    parity sqall $P || exit 1
+    bash tools/ab.sh "$TAG/ab_sqall_C1" "base sqall sqall base base sqall" || exit 1
+    bash tools/ab.sh "$TAG/ab_sqall_C3" "base sqall sqall base" --config C3 || exit 1 ;;
   *) echo "unknown experiment $EXP"; exit 2 ;;
 esac
 echo ok

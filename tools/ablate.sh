@@ -151,6 +151,7 @@ declare -A V=(
   [lg12]="$COMMON $DEV -DOM_ACC_GROUP=8 -DOM_WF_LATE_GLOBAL=12"
   # r03: march SDF roots as hipcc's sqrt core when the whole wave is in range (same bits)
   [sqcore]="$COMMON $DEV -DOM_MARCH_SQRT_CORE=1"
+  [sqall]="$COMMON $DEV -DOM_SQRT_CORE=1"
   # r03: non-temporal hints on the path-state loads / stores (component loads, same registers)
   [ntl]="$COMMON $DEV -DOM_WF_NT_LOADS=1 -DOM_WF_NT_STORES=0"
   [nt0]="$COMMON $DEV -DOM_WF_NT_LOADS=0 -DOM_WF_NT_STORES=0"
