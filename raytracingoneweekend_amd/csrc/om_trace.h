@@ -220,11 +220,38 @@ __device__ __forceinline__ void offer_uniform(const OmSceneDev& S, uint32_t gi, 
 #ifndef OM_DIAG_SPHERE
 #define OM_DIAG_SPHERE 1
 #endif
+// OM_A2_PRELOAD: with at most 4 always2 records (every reference scene), all of them are loaded
+// up front (their scalar loads in flight together) and the loop is unrolled, so each record's
+// test no longer starts with a dependent s_load round trip.
+#ifndef OM_A2_PRELOAD
+#define OM_A2_PRELOAD 0
+#endif
+template <class Wk>
+__device__ __forceinline__ void offer_always2_one(const OmSceneDev& S, const OmAlwaysRec& A, F3 o, F3 d, float tmin, float ix,
+                                                  float iy, float iz, float nox, float noy, float noz, float t_lo,
+                                                  float& closest, int& best, Wk& w);
 template <class Wk>
 __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, float tmin, float ix, float iy, float iz,
                                               float nox, float noy, float noz, float t_lo, float& closest, int& best, Wk& w) {
-    for (uint32_t k = 0; k < S.n_always2; ++k) {
-        const OmAlwaysRec A = uniform_load(S.always2_rec + k);
+#if OM_A2_PRELOAD
+    if (S.n_always2 <= 4u) {
+        OmAlwaysRec A[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k) if (k < S.n_always2) A[k] = uniform_load(S.always2_rec + k);
+#pragma unroll
+        for (uint32_t k = 0; k < 4u; ++k)
+            if (k < S.n_always2) offer_always2_one(S, A[k], o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
+        return;
+    }
+#endif
+    for (uint32_t k = 0; k < S.n_always2; ++k)
+        offer_always2_one(S, uniform_load(S.always2_rec + k), o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
+}
+template <class Wk>
+__device__ __forceinline__ void offer_always2_one(const OmSceneDev& S, const OmAlwaysRec& A, F3 o, F3 d, float tmin, float ix,
+                                                  float iy, float iz, float nox, float noy, float noz, float t_lo,
+                                                  float& closest, int& best, Wk& w) {
+    {
 #ifndef OM_ALWAYS2_INF_SLAB
         // an unbounded record (huge primitives, planes: lo = -inf) passes every slab test
         if (A.lo[0] == -INFINITY) {
@@ -235,11 +262,11 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
                 if (sphere_root_diag(uniform_load(S.sph_test + A.gi), o, d, tmin, closest, t) && (t < closest || (int)A.gi > best)) {
                     closest = t; best = (int)A.gi;
                 }
-                continue;
+                return;
             }
 #endif
             offer_uniform(S, A.gi, o, d, tmin, closest, best, w);
-            continue;
+            return;
         }
 #endif
         w.add_pre();

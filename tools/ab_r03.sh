@@ -3,7 +3,7 @@
 # _abl/; build them first with `VARIANTS="..." bash tools/ablate.sh build`).  Each run checks the
 # candidate build's parity through OM_LIB where it changes code, then alternates the variants.
 #   bash tools/ab_r03.sh EXPERIMENT [TAG]      -> gpurun_out/TAG/...
-# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio | sqall
+# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio | sqall | a2p
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -74,6 +74,10 @@ case $EXP in
     parity sqall $P || exit 1
     bash tools/ab.sh "$TAG/ab_sqall_C1" "base sqall sqall base base sqall" || exit 1
     bash tools/ab.sh "$TAG/ab_sqall_C3" "base sqall sqall base" --config C3 || exit 1 ;;
+  a2p)          # the always2 records loaded up front (C1, C3)
+    parity a2p $P || exit 1
+    bash tools/ab.sh "$TAG/ab_a2p_C1" "base a2p a2p base base a2p" || exit 1
+    bash tools/ab.sh "$TAG/ab_a2p_C3" "base a2p a2p base" --config C3 || exit 1 ;;
   *) echo "unknown experiment $EXP"; exit 2 ;;
 esac
 echo ok

@@ -152,6 +152,8 @@ declare -A V=(
   # r03: march SDF roots as hipcc's sqrt core when the whole wave is in range (same bits)
   [sqcore]="$COMMON $DEV -DOM_MARCH_SQRT_CORE=1"
   [sqall]="$COMMON $DEV -DOM_SQRT_CORE=1"
+  # r03: the always2 records loaded up front (unrolled, <= 4 records)
+  [a2p]="$COMMON $DEV -DOM_A2_PRELOAD=1"
   # r03: non-temporal hints on the path-state loads / stores (component loads, same registers)
   [ntl]="$COMMON $DEV -DOM_WF_NT_LOADS=1 -DOM_WF_NT_STORES=0"
   [nt0]="$COMMON $DEV -DOM_WF_NT_LOADS=0 -DOM_WF_NT_STORES=0"
