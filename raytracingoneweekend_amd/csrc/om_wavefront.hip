@@ -147,6 +147,9 @@ constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segme
 #endif
 constexpr uint32_t kTailSpbAsync = OM_WF_TAIL_SPB_ASYNC;
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
+// marched worlds: 12 (C2, 8 march steps per refill check, r03_v22/v23: T = 6 / 8 / 10 / 12 / 16 / 20
+// / 24 -> 2579 / 2647 / 2674 / 2668 / 2655 / 2605 / 2541 Msamples/s, means of two or four runs)
+constexpr uint32_t kTailMarched = 12;
 // Merged late bounces (traced worlds): from bounce OM_WF_MERGE_AT on (0: never), a bounce
 // workgroup handles OM_WF_MERGE consecutive queue segments.  The late bounces carry few paths
 // per segment, yet each launch filled every CU with whole 512-lane workgroups (8 wave slots
@@ -1298,7 +1301,8 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     const bool async_tail = OM_WF_ASYNC_TAIL && concurrent && ns >= 2u && 2u * ns <= (uint32_t)kMaxSets;
     const uint32_t nsets = async_tail ? std::min<uint32_t>(2u * ns, nb) : ns;
     const uint32_t depth_cap = L.P.max_depth > 1u ? L.P.max_depth : 1u;
-    const uint32_t tail_at = L.tail_bounce ? L.tail_bounce : kTailDefault;
+    const bool marched_world = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
+    const uint32_t tail_at = L.tail_bounce ? L.tail_bounce : (marched_world ? kTailMarched : kTailDefault);
     int dev = 0;
     (void)hipGetDevice(&dev);
     int cus = 256;

@@ -3,7 +3,7 @@
 # _abl/; build them first with `VARIANTS="..." bash tools/ablate.sh build`).  Each run checks the
 # candidate build's parity through OM_LIB where it changes code, then alternates the variants.
 #   bash tools/ab_r03.sh EXPERIMENT [TAG]      -> gpurun_out/TAG/...
-# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio | sqall | a2p
+# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio | sqall | a2p | tailC2 | tailC2b
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -78,6 +78,15 @@ case $EXP in
     parity a2p $P || exit 1
     bash tools/ab.sh "$TAG/ab_a2p_C1" "base a2p a2p base base a2p" || exit 1
     bash tools/ab.sh "$TAG/ab_a2p_C3" "base a2p a2p base" --config C3 || exit 1 ;;
+  tailC2)       # C2's tail threshold on the 8-steps-per-check k_march
+    bench_runs tail_sweep_C2.jsonl "C2 tail 12|--config C2 --tail 12" "C2 tail 16|--config C2 --tail 16" \
+        "C2 tail 20|--config C2 --tail 20" "C2 tail 24|--config C2 --tail 24" "C2 tail 24|--config C2 --tail 24" \
+        "C2 tail 20|--config C2 --tail 20" "C2 tail 16|--config C2 --tail 16" "C2 tail 12|--config C2 --tail 12" || exit 1 ;;
+  tailC2b)      # lower tail thresholds on C2
+    bench_runs tail_sweep_C2b.jsonl "C2 tail 6|--config C2 --tail 6" "C2 tail 8|--config C2 --tail 8" \
+        "C2 tail 10|--config C2 --tail 10" "C2 tail 12|--config C2 --tail 12" "C2 tail 16|--config C2 --tail 16" \
+        "C2 tail 16|--config C2 --tail 16" "C2 tail 12|--config C2 --tail 12" "C2 tail 10|--config C2 --tail 10" \
+        "C2 tail 8|--config C2 --tail 8" "C2 tail 6|--config C2 --tail 6" || exit 1 ;;
   *) echo "unknown experiment $EXP"; exit 2 ;;
 esac
 echo ok
