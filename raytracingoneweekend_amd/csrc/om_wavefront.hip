@@ -150,6 +150,9 @@ constexpr uint32_t kTailDefault = 16;                             // first bounc
 // marched worlds: 12 (C2, 8 march steps per refill check, r03_v22/v23: T = 6 / 8 / 10 / 12 / 16 / 20
 // / 24 -> 2579 / 2647 / 2674 / 2668 / 2655 / 2605 / 2541 Msamples/s, means of two or four runs)
 constexpr uint32_t kTailMarched = 12;
+// BVH2s read through L2 (S-10k): 10 (C3, r03_v24/v25: T = 6 / 8 / 10 / 12 / 16 / 20 -> 3318 / 3523 /
+// 3553 / 3517 / 3416 / 3351 Msamples/s, means of two to four runs)
+constexpr uint32_t kTailL2 = 10;
 // Merged late bounces (traced worlds): from bounce OM_WF_MERGE_AT on (0: never), a bounce
 // workgroup handles OM_WF_MERGE consecutive queue segments.  The late bounces carry few paths
 // per segment, yet each launch filled every CU with whole 512-lane workgroups (8 wave slots
@@ -1301,8 +1304,6 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     const bool async_tail = OM_WF_ASYNC_TAIL && concurrent && ns >= 2u && 2u * ns <= (uint32_t)kMaxSets;
     const uint32_t nsets = async_tail ? std::min<uint32_t>(2u * ns, nb) : ns;
     const uint32_t depth_cap = L.P.max_depth > 1u ? L.P.max_depth : 1u;
-    const bool marched_world = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
-    const uint32_t tail_at = L.tail_bounce ? L.tail_bounce : (marched_world ? kTailMarched : kTailDefault);
     int dev = 0;
     (void)hipGetDevice(&dev);
     int cus = 256;
@@ -1318,6 +1319,8 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     // segments, a multiple of the tail grouping: 4096 lanes per CU (8 workgroups of 512) for
     // traced worlds whose BVH2 sits in LDS, 8192 for marched worlds and L2-resident trees
     const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
+    const uint32_t tail_at = L.tail_bounce ? L.tail_bounce
+                           : march ? kTailMarched : tr == TR_BVH2_GLOBAL ? kTailL2 : kTailDefault;
     const uint32_t lanes_per_cu = (march || tr == TR_BVH2_GLOBAL) ? OM_WF_LANES_PER_CU_WIDE : OM_WF_LANES_PER_CU;
     uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (lanes_per_cu / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;

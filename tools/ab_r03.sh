@@ -3,7 +3,7 @@
 # _abl/; build them first with `VARIANTS="..." bash tools/ablate.sh build`).  Each run checks the
 # candidate build's parity through OM_LIB where it changes code, then alternates the variants.
 #   bash tools/ab_r03.sh EXPERIMENT [TAG]      -> gpurun_out/TAG/...
-# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio | sqall | a2p | tailC2 | tailC2b
+# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio | sqall | a2p | tailC2 | tailC2b | tailC3 | tailC3b
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -87,6 +87,14 @@ case $EXP in
         "C2 tail 10|--config C2 --tail 10" "C2 tail 12|--config C2 --tail 12" "C2 tail 16|--config C2 --tail 16" \
         "C2 tail 16|--config C2 --tail 16" "C2 tail 12|--config C2 --tail 12" "C2 tail 10|--config C2 --tail 10" \
         "C2 tail 8|--config C2 --tail 8" "C2 tail 6|--config C2 --tail 6" || exit 1 ;;
+  tailC3)       # C3's tail threshold (BVH2 through L2)
+    bench_runs tail_sweep_C3.jsonl "C3 tail 12|--config C3 --tail 12" "C3 tail 16|--config C3 --tail 16" \
+        "C3 tail 20|--config C3 --tail 20" "C3 tail 20|--config C3 --tail 20" "C3 tail 16|--config C3 --tail 16" \
+        "C3 tail 12|--config C3 --tail 12" || exit 1 ;;
+  tailC3b)      # lower tail thresholds on C3
+    bench_runs tail_sweep_C3b.jsonl "C3 tail 6|--config C3 --tail 6" "C3 tail 8|--config C3 --tail 8" \
+        "C3 tail 10|--config C3 --tail 10" "C3 tail 12|--config C3 --tail 12" "C3 tail 12|--config C3 --tail 12" \
+        "C3 tail 10|--config C3 --tail 10" "C3 tail 8|--config C3 --tail 8" "C3 tail 6|--config C3 --tail 6" || exit 1 ;;
   *) echo "unknown experiment $EXP"; exit 2 ;;
 esac
 echo ok
