@@ -245,7 +245,8 @@ enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1, OM_PIPELINE_AUTO =
 om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
 /* Wavefront pipeline: bounces >= `bounce` are finished by one persistent tail launch
  * (lanes run whole remaining paths); 0 = default (16; 12 for worlds with marched
- * primitives, 10 when the BVH2 is too big for LDS), >= max_depth = no tail.  A pure
+ * primitives, 10 when the BVH2 is too big for LDS, 24 for batches above 2^25 paths),
+ * >= max_depth = no tail.  A pure
  * scheduling knob: results are bit-identical for every value. */
 om_status om_set_tail_bounce(om_ctx* ctx, uint32_t bounce);
 

@@ -153,6 +153,10 @@ constexpr uint32_t kTailMarched = 12;
 // BVH2s read through L2 (S-10k): 10 (C3, r03_v24/v25: T = 6 / 8 / 10 / 12 / 16 / 20 -> 3318 / 3523 /
 // 3553 / 3517 / 3416 / 3351 Msamples/s, means of two to four runs)
 constexpr uint32_t kTailL2 = 10;
+// batches above 2^25 paths (C4's 4K frame: 16 spp = 133M paths) keep more paths per late bounce,
+// so the per-bounce launches stay efficient longer: 24 (C4, r03_v26: T = 12 / 16 / 20 / 24 ->
+// 6956 / 7240 / 7304 / 7374 Msamples/s, means of two runs)
+constexpr uint32_t kTailBigBatch = 24;
 // Merged late bounces (traced worlds): from bounce OM_WF_MERGE_AT on (0: never), a bounce
 // workgroup handles OM_WF_MERGE consecutive queue segments.  The late bounces carry few paths
 // per segment, yet each launch filled every CU with whole 512-lane workgroups (8 wave slots
@@ -1320,7 +1324,8 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     // traced worlds whose BVH2 sits in LDS, 8192 for marched worlds and L2-resident trees
     const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
     const uint32_t tail_at = L.tail_bounce ? L.tail_bounce
-                           : march ? kTailMarched : tr == TR_BVH2_GLOBAL ? kTailL2 : kTailDefault;
+                           : march ? kTailMarched : tr == TR_BVH2_GLOBAL ? kTailL2
+                           : max_paths > (1ull << 25) ? kTailBigBatch : kTailDefault;
     const uint32_t lanes_per_cu = (march || tr == TR_BVH2_GLOBAL) ? OM_WF_LANES_PER_CU_WIDE : OM_WF_LANES_PER_CU;
     uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (lanes_per_cu / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;

@@ -3,7 +3,7 @@
 # _abl/; build them first with `VARIANTS="..." bash tools/ablate.sh build`).  Each run checks the
 # candidate build's parity through OM_LIB where it changes code, then alternates the variants.
 #   bash tools/ab_r03.sh EXPERIMENT [TAG]      -> gpurun_out/TAG/...
-# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio | sqall | a2p | tailC2 | tailC2b | tailC3 | tailC3b
+# EXPERIMENT: kernel_c3 | merge | accstream | lateglobal | sqcore | nt | batch | batch2 | munroll | munroll2 | munroll3 | setprio | sqall | a2p | tailC2 | tailC2b | tailC3 | tailC3b | tailC4 | tailC4b
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -95,6 +95,14 @@ case $EXP in
     bench_runs tail_sweep_C3b.jsonl "C3 tail 6|--config C3 --tail 6" "C3 tail 8|--config C3 --tail 8" \
         "C3 tail 10|--config C3 --tail 10" "C3 tail 12|--config C3 --tail 12" "C3 tail 12|--config C3 --tail 12" \
         "C3 tail 10|--config C3 --tail 10" "C3 tail 8|--config C3 --tail 8" "C3 tail 6|--config C3 --tail 6" || exit 1 ;;
+  tailC4)       # C4's tail threshold (4K frame, 16-spp batches of 133M paths)
+    bench_runs tail_sweep_C4.jsonl "C4 tail 12|--config C4 --tail 12" "C4 tail 16|--config C4 --tail 16" \
+        "C4 tail 20|--config C4 --tail 20" "C4 tail 24|--config C4 --tail 24" "C4 tail 24|--config C4 --tail 24" \
+        "C4 tail 20|--config C4 --tail 20" "C4 tail 16|--config C4 --tail 16" "C4 tail 12|--config C4 --tail 12" || exit 1 ;;
+  tailC4b)      # higher tail thresholds on C4
+    bench_runs tail_sweep_C4b.jsonl "C4 tail 24|--config C4 --tail 24" "C4 tail 28|--config C4 --tail 28" \
+        "C4 tail 32|--config C4 --tail 32" "C4 tail 32|--config C4 --tail 32" "C4 tail 28|--config C4 --tail 28" \
+        "C4 tail 24|--config C4 --tail 24" || exit 1 ;;
   *) echo "unknown experiment $EXP"; exit 2 ;;
 esac
 echo ok
