@@ -90,6 +90,12 @@ BYTES_PER_SAMPLE = 32
 BYTES_PER_SEGMENT_SPLIT = 128 + 32 + 16
 BOUNCE_FAMILY = ("bounce0", "bounce", "tail")            # trace+shade launches (+ k_raygen/k_march: split)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")          # C1; other configs: pmc_traffic_<config>.json
+# per-kernel PMC summaries of the same bench command (tools/pmc_final.sh -> tools/pmc_summary.py),
+# committed per config: the roofline carries the family's VALU lane utilisation and wait fraction
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary_{}.json")
+# bench.py's window parity (after the timed region, untimed): the oracle renders one window of the
+# timed frame in the cpu_baseline subprocess (oracle/cpu_bench.py --window), compared byte for byte
+WINDOW = {"C1": 16, "C2": 16, "C3": 8, "C4": 16}
 
 
 def cpu_baseline(cfg, budget_s, lib="liboro.so", threads=0, dump=None):
@@ -106,6 +112,54 @@ def cpu_baseline(cfg, budget_s, lib="liboro.so", threads=0, dump=None):
     if r.returncode != 0:
         raise RuntimeError(f"cpu baseline {cfg}/{lib} failed: {r.stderr[-2000:]}")
     return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def pmc_fields(name):
+    """VALU lane utilisation and wait fractions of the bounce family from the committed per-kernel
+    PMC summary of this config ("also report ... VALU utilization"), or None."""
+    f = PMC_SUMMARY.format(name)
+    if not os.path.exists(f):
+        return None
+    pm = json.load(open(f))
+    comb = pm["combined"]["derived"]
+    per = {k: {"valu_lane_utilisation": round(v["derived"]["valu_lane_utilisation"], 4),
+               "wait_any_frac": round(v["derived"]["wait_any_frac"], 4),
+               "wave_cycle_share": None}
+           for k, v in pm["kernels"].items() if "valu_lane_utilisation" in v.get("derived", {})}
+    # a kernel's share of the family's wave-cycles: mean per dispatch x dispatches
+    wc = {k: v["counters"].get("SQ_WAVE_CYCLES", 0.0) * v["dispatches"].get("SQ_WAVE_CYCLES", 0)
+          for k, v in pm["kernels"].items()}
+    tot = sum(wc.values()) or 1.0
+    for k in per:
+        per[k]["wave_cycle_share"] = round(wc.get(k, 0.0) / tot, 4)
+    return {"valu_lane_utilisation": round(comb["valu_lane_utilisation"], 4),
+            "wait_any_frac": round(comb["wait_any_frac"], 4), "wait_inst_frac": round(comb["wait_inst_frac"], 4),
+            "per_kernel": per, "source": pm.get("source"), "file": os.path.relpath(f, ROOT)}
+
+
+def window_parity(name, frame_u8, W, H, spp, depth, march_steps):
+    """One window of the timed frame (rank 0, after the timed region) vs the oracle's render of it
+    (oracle/cpu_bench.py --window in a child process: the oracle never enters this process)."""
+    import tempfile
+    size = WINDOW[name]
+    x0, y0 = W // 2 - size // 2, H // 2 - size // 2
+    with tempfile.TemporaryDirectory() as td:
+        dump = os.path.join(td, "window.npy")
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_bench.py"), "--config", name,
+                            "--window", f"{W},{H},{x0},{y0},{size},{spp}", "--dump", dump, "--threads", "-1"],
+                           capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"oracle window {name} failed: {r.stderr[-2000:]}")
+        info = json.loads(r.stdout.strip().splitlines()[-1])
+        exp = np.load(dump, allow_pickle=False).view(np.uint8).reshape(-1, 40)
+    pix = ((np.arange(y0, y0 + size)[:, None] * W) + np.arange(x0, x0 + size)[None, :]).reshape(-1)
+    got = frame_u8.reshape(W * H, 40)[pix]
+    bad = int(np.any(got != exp, axis=1).sum())
+    if bad:
+        print(f"bench: {name} window parity FAILED: {bad}/{pix.size} pixels differ from the oracle", file=sys.stderr)
+    return {"window": [int(x0), int(y0), size], "spp": spp, "depth": depth, "pixels": int(pix.size),
+            "bit_exact_vs_oracle": bad == 0, "pixels_differ": bad, "oracle_s": info["seconds"],
+            "objects_hit": int(np.count_nonzero(got.view(np.uint64)[:, 0]))}
 
 
 class Control:
@@ -159,6 +213,7 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
     L.check(L.lib.om_set_streams(ctx, args.streams), ctx)
     L.check(L.lib.om_set_primary_lists(ctx, {"off": 0, "auto": 1, "on": 2}[args.primary_lists]), ctx)
     comm = shard.Comm(ctx, n, rank, ctl.unique_id())
+    nranks_seen = check_comm_ranks(comm.info(), n, rank)     # RCCL's own view of the communicator
     spp_step = spp_per_step * (1 if name == "C4" else n)          # C4: fixed frame; else fixed per-GPU work
     spp_total = spp_step * steps
     cap = shard.shard_capacity(W, H, n)
@@ -208,11 +263,14 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
     host = sh.cpu().numpy().copy()
     mine = host[: n_mine * 40].view(L.PIXEL_STATS_DTYPE)
     assert int(mine["n"].min()) == spp_total and int(mine["n"].max()) == spp_total, "every pixel must take every sample"
+    parity = None
     if rank == 0:
         fr = frame.cpu().numpy().view(L.PIXEL_STATS_DTYPE)
         assert int(fr["n"].min()) == spp_total and int(fr["n"].max()) == spp_total, "gathered frame incomplete"
         assert np.array_equal(fr[shard.tile_pixels(W, H, 0, n)].view(np.uint8).reshape(-1), host[: n_mine * 40]), \
             "gathered frame differs from rank 0's shard"
+        if not args.no_window_parity:
+            parity = window_parity(name, fr.view(np.uint8), W, H, spp_total, depth, cfg["march_steps"])
 
     # per-launch durations (untimed): the same K steps again, production build, every launch
     # bracketed by events on its stream (om_set_timing 1) -> the rocprof-comparable average
@@ -273,6 +331,7 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
         if pmc_ok and os.path.exists(pmc_file) and not mega and args.kernel == "auto":
             pm = json.load(open(pmc_file))
             traffic, traffic_src = pm["hbm_bytes_per_launch"], pm["source"]
+        pmc = pmc_fields(name) if (pmc_ok and not mega and args.kernel == "auto") else None
         roof = {"bound": "valu", "achieved": round(achieved_tflops, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": traffic,
                 "issue_peak": ISSUE_PEAK_TFLOPS, "frac_of_issue_peak": round(achieved_tflops / ISSUE_PEAK_TFLOPS, 4),
@@ -287,17 +346,36 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
                 "hbm_achieved_gbs": round(nbytes / span_s / 1e9, 2), "traffic_source": traffic_src,
                 "traffic_over_algorithmic": round(traffic / (nbytes / launches), 3) if traffic else None,
                 "kernel_share_of_step": round(span_s / elapsed, 4), "timing": timing_mode,
+                "valu_lane_utilisation": pmc["valu_lane_utilisation"] if pmc else None,
+                "wait_any_frac": pmc["wait_any_frac"] if pmc else None, "pmc": pmc,
                 "all_kernels_ms_per_step": {k: round(kl.ms[i] / steps, 4) for i, k in enumerate(L.KT_CLASSES)
                                             if kl.launches[i]}}
     return {
         "value": round(value, 3), "elapsed_s": elapsed, "steps": steps, "W": W, "H": H, "depth": depth,
         "spp_total": spp_total, "spp_step": spp_step, "mega": mega, "roofline": roof,
+        "window_parity": parity, "nranks_seen": nranks_seen,
         "work": {"segments_per_sample": round(ctr.segments / max(1, ctr.samples), 4),
                  "prim_tests_per_segment": round(ctr.prim_tests / max(1, ctr.segments), 3),
                  "box_tests_per_segment": round(ctr.pre_tests / max(1, ctr.segments), 3),
                  "march_steps_per_segment": round(ctr.march_steps / max(1, ctr.segments), 3),
                  "gsegments_per_s": round(ctr.segments * n / elapsed / 1e9, 4)},
     }
+
+
+def check_comm_ranks(seen, world_size, rank):
+    """RCCL's (nranks, rank) for the bench's communicator must be the launcher's (WORLD_SIZE, RANK):
+    a silently smaller communicator would time a fraction of the job.  Returns nranks."""
+    n_seen, r_seen = seen
+    if n_seen != world_size or r_seen != rank:
+        raise SystemExit(f"bench: RCCL communicator has {n_seen} ranks (this is rank {r_seen}), "
+                         f"but WORLD_SIZE={world_size} RANK={rank}")
+    return n_seen
+
+
+def config_entry(name, e, note=""):
+    return {"metric": "Msamples/s", "value": e["value"], "ms_per_step": round(e["elapsed_s"] / e["steps"] * 1e3, 4),
+            "workload": workload(name, e) + note, "pipeline": "megakernel" if e["mega"] else "wavefront",
+            "roofline": e["roofline"], "work": e["work"], "window_parity": e["window_parity"]}
 
 
 def workload(name, r):
@@ -327,6 +405,8 @@ def main():
                     help="quick mode: the headline config only (no CPU baselines, no `configs` block)")
     ap.add_argument("--no-extras", action="store_true", help="no `configs` block (C2/C3/C0) at N=1")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-window-parity", action="store_true",
+                    help="skip the oracle window of each timed frame (untimed; a few seconds of host CPU)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
 
@@ -346,21 +426,22 @@ def main():
     quick = args.no_cpu_baseline or args.no_extras
     if rank == 0 and world_size == 1 and not quick and args.config == "C1":
         extras = {}
+        # C1_frame: exactly the quoted "1080p@512spp" frame, one fresh frame of 4 x 128-spp calls
+        # timed alone (its end-of-call drains included), beside the driver's --steps run
+        c1 = CONFIGS["C1"]
+        e = run_config("C1", args, ctl, local_rank, c1["spp"] // args.spp_per_step, 1, args.spp_per_step, "region")
+        extras["C1_frame"] = config_entry("C1", e, " (one fresh 512-spp frame)")
+        extras["C1_frame"]["ms_per_frame"] = round(e["elapsed_s"] * 1e3, 4)
         for name in ("C2", "C3"):
             c = CONFIGS[name]
             e = run_config(name, args, ctl, local_rank, c["spp"] // args.spp_per_step, 1, args.spp_per_step, "region")
-            extras[name] = {"metric": "Msamples/s", "value": e["value"], "ms_per_step": round(e["elapsed_s"] / e["steps"] * 1e3, 4),
-                            "workload": workload(name, e), "pipeline": "megakernel" if e["mega"] else "wavefront",
-                            "roofline": e["roofline"], "work": e["work"],
-                            "cpu_baseline": cpu_baseline(name, min(8.0, args.cpu_budget))}
+            extras[name] = config_entry(name, e)
+            extras[name]["cpu_baseline"] = cpu_baseline(name, min(8.0, args.cpu_budget))
         # C4's 4K frame at N=1: 256 of the config's 4096 spp (the full frame is the multi-GPU run,
         # --config C4), so the driver's line exercises the 3840x2160 frame too
         e = run_config("C4", args, ctl, local_rank, max(1, 256 // args.spp_per_step), 1, args.spp_per_step, "region")
-        extras["C4"] = {"metric": "Msamples/s", "value": e["value"], "ms_per_step": round(e["elapsed_s"] / e["steps"] * 1e3, 4),
-                        "workload": workload("C4", e) + " (N=1 leg of the 8-GPU config: 256 of its 4096 spp)",
-                        "pipeline": "megakernel" if e["mega"] else "wavefront",
-                        "roofline": e["roofline"], "work": e["work"],
-                        "cpu_baseline": cpu_baseline("C4", min(6.0, args.cpu_budget))}
+        extras["C4"] = config_entry("C4", e, " (N=1 leg of the 8-GPU config: 256 of its 4096 spp)")
+        extras["C4"]["cpu_baseline"] = cpu_baseline("C4", min(6.0, args.cpu_budget))
         extras["C0"] = run_c0(args)
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
@@ -391,6 +472,8 @@ def main():
                        "pipeline": args.pipeline + (("->megakernel" if r["mega"] else "->wavefront")
                                                     if args.pipeline == "auto" else ""),
                        "tail_bounce": args.tail or "default", "streams": args.streams},
+            "nranks_seen": r["nranks_seen"],
+            "window_parity": r["window_parity"],
             "hbm_gbs": r["roofline"]["hbm_achieved_gbs"] if r["roofline"] else None,
             "roofline": r["roofline"],
             "work": r["work"],

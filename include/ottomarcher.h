@@ -347,6 +347,9 @@ om_status om_comm_unique_id(uint8_t id[OM_COMM_ID_BYTES]);
 om_status om_comm_init_rank(om_ctx* ctx, uint32_t nranks, uint32_t rank, const uint8_t id[OM_COMM_ID_BYTES],
                             om_comm** out);
 void om_comm_destroy(om_comm* comm);
+/* What RCCL itself reports for this communicator: its rank count (ncclCommCount) and this
+ * rank (ncclCommUserRank).  A host checks them against its own world size before timing. */
+om_status om_comm_info(const om_comm* comm, int32_t* nranks, int32_t* rank);
 /* Renders this rank's tiles into dev_shard (om_shard_capacity entries of device memory on
  * the comm's device, list order), like om_render_device on those pixels.  Asynchronous. */
 om_status om_render_shard(om_comm* comm, const om_camera* cam, const om_render_params* p, om_pixel_stats* dev_shard,
@@ -389,10 +392,10 @@ om_status om_multi_render(om_multi* m, const om_camera* cam, const om_render_par
 om_status om_multi_gather(om_multi* m, om_pixel_stats* dev_frame, uint32_t width, uint32_t height, void* stream);
 /* Forget the resident frame: the next om_multi_render deals its frame out again. */
 void om_multi_reset(om_multi* m);
-/* Host framebuffer form (like om_render): `stats` (W*H, caller-owned host memory) is copied
- * to devices[0] and dealt out when the call sees this buffer first (as above; om_multi_reset
- * after writing it yourself); every call renders across the ranks, gathers once and copies the
- * frame back; synchronous.  `counters` (optional) sums every rank's work counters of this call. */
+/* Host framebuffer form (like om_render): every call copies `stats` (W*H, caller-owned host
+ * memory, which the caller may have zeroed or rewritten since the last call) to devices[0],
+ * deals it out, renders across the ranks, gathers once and copies the frame back; synchronous.
+ * `counters` (optional) sums every rank's work counters of this call. */
 om_status om_multi_render_host(om_multi* m, const om_camera* cam, const om_render_params* p, om_pixel_stats* stats,
                                om_counters* counters);
 const char* om_multi_last_error(const om_multi* m);

@@ -400,7 +400,6 @@ public:
         if (!pixels_box.pixels || pixels_box.pixels->size() != image_size)
             throw Error(OM_ERR_INVALID, "ottomarcher: MultiFrame::render: pixels must hold image_width*image_height entries");
         const uint32_t per_call = opt.samples_per_call ? opt.samples_per_call : samples_per_pixel;
-        om_multi_reset(m_);                 // deal the caller's framebuffer out once, on the first call
         for (uint32_t done = 0; done < samples_per_pixel; done += per_call) {
             om_render_params p{};
             p.width = image_width; p.height = image_height; p.spp_total = samples_per_pixel; p.sample_begin = done;

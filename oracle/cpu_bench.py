@@ -6,6 +6,10 @@ budget is spent, and prints one JSON object.  Which build is timed is chosen by 
 this as a subprocess once per build.
 
     ORO_LIB=liboro_v3.so python oracle/cpu_bench.py --config C1 --budget 12 [--threads N]
+
+With --window W,H,X0,Y0,SIZE,SPP it instead renders the SIZE x SIZE window at (X0, Y0) of the
+config's W x H frame at SPP samples (render seed 1) and saves its Stats to --dump: the oracle side
+of bench.py's per-config window parity check (the GPU frame it times vs this restatement).
 """
 import argparse
 import json
@@ -99,6 +103,16 @@ def run(cfg, budget_s, threads, spp_total=64, seed=1, dump=None):
                       f"{threads} threads ({os.path.basename(O.LIB)}), {t_total:.1f} s"}
 
 
+def window(cfg, spec, threads, dump, seed=1):
+    """The oracle's Stats of one window of the config's frame (bench.py's window parity)."""
+    w, h, x0, y0, size, spp = (int(v) for v in spec.split(","))
+    p = O.params(w, h, spp, max_depth=DEPTH.get(cfg, 50), seed=seed, march_steps=MARCH.get(cfg, 1024))
+    t0 = time.perf_counter()
+    st = O.render_pixels(scene(cfg), O.default_camera(w / h), p, O.window_pixels(w, h, x0, y0, size), nthreads=threads)
+    np.save(dump, st, allow_pickle=False)
+    return {"seconds": round(time.perf_counter() - t0, 3), "threads": threads, "window": [x0, y0, size], "spp": spp}
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--config", default="C1", choices=list(SCENES))
@@ -106,7 +120,11 @@ if __name__ == "__main__":
     ap.add_argument("--threads", type=int, default=0,
                     help="0: num_cpus::get() - 1 as main.rs:170; -1: num_cpus::get() (the all-cores point)")
     ap.add_argument("--dump", default=None, help="save the rendered Stats (.npy) here")
+    ap.add_argument("--window", default=None, help="W,H,X0,Y0,SIZE,SPP: render one window into --dump")
     a = ap.parse_args()
     n = num_cpus()[0]
     t = a.threads if a.threads > 0 else (n if a.threads < 0 else max(1, n - 1))
-    print(json.dumps(run(a.config, a.budget, t, dump=a.dump)))
+    if a.window:
+        print(json.dumps(window(a.config, a.window, t, a.dump)))
+    else:
+        print(json.dumps(run(a.config, a.budget, t, dump=a.dump)))

@@ -1100,4 +1100,24 @@ void oro_render_pixels(void* wp, const OroCamera* c, const RenderParams* p, void
     for (uint32_t k = 0; k < n; ++k) render_pixel(*w, cam, *p, jt.data(), skey, pixels[k], stats[k], ctr);
 }
 
+// The same over `nthreads` workers (pixel k to worker k % nthreads): pixels are independent, so
+// the stats are those of the single-thread form.  Used for oracle windows of full-size frames.
+void oro_render_pixels_mt(void* wp, const OroCamera* c, const RenderParams* p, void* stats_v, const uint32_t* pixels,
+                          uint32_t n, int32_t nthreads) {
+    World* w = (World*)wp; w->assign_ids(); w->march_steps = p->march_steps;
+    Camera cam = cam_from(c);
+    PixelStats* stats = (PixelStats*)stats_v;
+    std::vector<float> jt = jitter_table(p->seed, p->spp_total);
+    uint64_t skey = seed_key(p->seed);
+    if (nthreads <= 0) { unsigned hc = std::thread::hardware_concurrency(); nthreads = hc > 0 ? (int32_t)hc : 1; }
+    auto worker = [&](int32_t tid) {
+        Counters ctr{0, 0, 0};
+        for (uint32_t k = (uint32_t)tid; k < n; k += (uint32_t)nthreads)
+            render_pixel(*w, cam, *p, jt.data(), skey, pixels[k], stats[k], ctr);
+    };
+    std::vector<std::thread> th;
+    for (int32_t t = 0; t < nthreads; ++t) th.emplace_back(worker, t);
+    for (auto& t : th) t.join();
+}
+
 }  // extern "C"

@@ -77,6 +77,8 @@ def _load():
         "oro_render": (None, [vp, C.POINTER(OroCamera), C.POINTER(OroParams), vp, C.c_int32, C.POINTER(C.c_uint64)]),
         "oro_render_pixels": (None, [vp, C.POINTER(OroCamera), C.POINTER(OroParams), vp, C.POINTER(C.c_uint32),
                                      C.c_uint32]),
+        "oro_render_pixels_mt": (None, [vp, C.POINTER(OroCamera), C.POINTER(OroParams), vp, C.POINTER(C.c_uint32),
+                                        C.c_uint32, C.c_int32]),
     }
     for n, (r, a) in sig.items():
         f = getattr(lib, n)
@@ -217,13 +219,24 @@ def render(world, cam, p, stats=None, nthreads=0):
     return stats, {"samples": ctr[0], "segments": ctr[1], "credited": ctr[2]}
 
 
-def render_pixels(world, cam, p, pixels):
-    """Render only `pixels` (uint32 row-major indices); returns compact stats[len(pixels)]."""
+def render_pixels(world, cam, p, pixels, nthreads=1):
+    """Render only `pixels` (uint32 row-major indices); returns compact stats[len(pixels)].
+    nthreads > 1 (0 = every hardware thread) spreads the pixels over workers: same bits."""
     pixels = np.ascontiguousarray(pixels, dtype=np.uint32)
     stats = np.zeros(pixels.size, dtype=PIXEL_STATS_DTYPE)
-    lib.oro_render_pixels(world.h, C.byref(cam), C.byref(p), stats.ctypes.data_as(C.c_void_p),
-                          pixels.ctypes.data_as(C.POINTER(C.c_uint32)), pixels.size)
+    if nthreads == 1:
+        lib.oro_render_pixels(world.h, C.byref(cam), C.byref(p), stats.ctypes.data_as(C.c_void_p),
+                              pixels.ctypes.data_as(C.POINTER(C.c_uint32)), pixels.size)
+    else:
+        lib.oro_render_pixels_mt(world.h, C.byref(cam), C.byref(p), stats.ctypes.data_as(C.c_void_p),
+                                 pixels.ctypes.data_as(C.POINTER(C.c_uint32)), pixels.size, int(nthreads))
     return stats
+
+
+def window_pixels(W, H, x0, y0, size):
+    """Row-major indices of the size x size window at (x0, y0)."""
+    ys, xs = np.meshgrid(np.arange(y0, y0 + size), np.arange(x0, x0 + size), indexing="ij")
+    return (ys * W + xs).reshape(-1).astype(np.uint32)
 
 
 def rng_draws(state, n):

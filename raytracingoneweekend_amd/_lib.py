@@ -75,7 +75,7 @@ EXPORTS = [
     "om_set_tail_bounce", "om_set_streams", "om_set_timing", "om_get_kernel_times", "om_display_device", "om_display",
     "om_write_bmp", "om_write_ppm", "om_set_primary_lists",
     "om_shard_capacity", "om_shard_pixels", "om_shard_assemble_host", "om_comm_unique_id", "om_comm_init_rank",
-    "om_comm_destroy", "om_render_shard", "om_gather_frame", "om_scatter_frame", "om_multi_create",
+    "om_comm_destroy", "om_comm_info", "om_render_shard", "om_gather_frame", "om_scatter_frame", "om_multi_create",
     "om_multi_destroy", "om_multi_transport", "om_multi_ctx", "om_multi_upload_world", "om_multi_render",
     "om_multi_last_error", "om_progress", "om_reset_progress", "om_host_register", "om_host_unregister",
     "om_multi_render_host", "om_multi_gather", "om_multi_reset", "om_rccl_library",
@@ -189,6 +189,7 @@ def _load():
         "om_multi_gather": (st, [vp, vp, C.c_uint32, C.c_uint32, vp]),
         "om_multi_reset": (None, [vp]),
         "om_rccl_library": (st, [C.c_char_p, C.c_uint32, C.POINTER(C.c_int32)]),
+        "om_comm_info": (st, [vp, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)

@@ -267,7 +267,12 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     // at most 15 records (S-traced: 485 records, leaves <= 8), a leaf child's 16-bit code is
     // OM_LEAF | first << 4 | count, so the traversal needs no leaf-table read to enter a leaf;
     // the table is still emitted (same order) for the other consumers.
-    const bool direct = OM_B2_DIRECT && fw.srecs.size() < 2048u;
+    // (both conditions checked here, not assumed from the builder's leaf cap: a count above 15
+    // would spill into the `first` bits)
+    int32_t max_leaf = 0;
+    for (const OmBvhNode& n : b.nodes)
+        if (n.left < 0) max_leaf = std::max(max_leaf, n.right);
+    const bool direct = OM_B2_DIRECT && fw.srecs.size() < 2048u && max_leaf <= 15;
     struct Emit2 {
         const Builder& b; const std::vector<uint32_t>& leaf_first; std::vector<OmBvh2Node>& out;
         std::vector<uint32_t>& leaves;

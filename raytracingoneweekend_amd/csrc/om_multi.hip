@@ -204,6 +204,16 @@ void om_comm_destroy(om_comm* c) {
     delete c;
 }
 
+om_status om_comm_info(const om_comm* c, int32_t* nranks, int32_t* rank) {
+    if (!c || !nranks || !rank) return omi::global_error(OM_ERR_INVALID, "om_comm_info: null argument");
+    int n = 0, r = 0;
+    ncclResult_t e = ncclCommCount(c->nc, &n);
+    if (e == ncclSuccess) e = ncclCommUserRank(c->nc, &r);
+    if (e != ncclSuccess) return omi::ctx_error(c->ctx, OM_ERR_DEVICE, nccl_msg("om_comm_info", e));
+    *nranks = n; *rank = r;
+    return OM_OK;
+}
+
 om_status om_render_shard(om_comm* c, const om_camera* cam, const om_render_params* p, om_pixel_stats* dev_shard, void* stream) {
     if (!c || !p) return omi::global_error(OM_ERR_INVALID, "om_render_shard: null argument");
     om_status s = check_frame(c->ctx, p->width, p->height);
@@ -296,11 +306,10 @@ struct om_multi {
     std::vector<hipEvent_t> ev;         // [0] on devices[0]: frame cut / gather done; [r]: rank r's stream
     bool ev0_live = false;              // ev[0] has been recorded (the ranks' streams wait on it)
     hipEvent_t done0 = nullptr;         // on devices[0]: rank 0's last render
+    bool renders_live = false;          // done0 and ev[r >= 1] have been recorded by a render
     const void* bound = nullptr;        // the device frame whose shards are resident
     uint32_t bw = 0, bh = 0;
     DBuf host_frame;                    // om_multi_render_host: the frame on devices[0]
-    const void* host_bound = nullptr;   // the host framebuffer host_frame mirrors
-    size_t host_bytes = 0;
     std::string err;
 };
 
@@ -366,11 +375,19 @@ om_status fence_from_root(om_multi* m, const std::vector<hipStream_t>& st) {
 }
 
 // Rank 0 cuts dev_frame into the shards (its own in place, the others' into staging) and deals
-// them out: the frame becomes the resident one.
+// them out: the frame becomes the resident one.  The shards and staging buffers it overwrites
+// may still be in use by the previous frame's work: every rank's last render (a frame re-dealt
+// with no gather in between: render(A), render(B)) and the last gather's reads of staging, on
+// whatever stream those calls were given.  So st[0] first waits on all of them.
 om_status deal_frame(om_multi* m, const om_pixel_stats* dev_frame, const std::vector<hipStream_t>& st) {
     const uint32_t N = (uint32_t)m->ctx.size();
     const Deal& D = m->deal;
     OM_MHIP(m, hipSetDevice(m->dev[0]));
+    if (m->renders_live) {
+        OM_MHIP(m, hipStreamWaitEvent(st[0], m->done0, 0));
+        for (uint32_t r = 1; r < N; ++r) OM_MHIP(m, hipStreamWaitEvent(st[0], m->ev[r], 0));
+    }
+    if (m->ev0_live) OM_MHIP(m, hipStreamWaitEvent(st[0], m->ev[0], 0));
     for (uint32_t r = 0; r < N; ++r)
         OM_MHIP(m, launch_move(false, dev_frame, D.list(r), D.count[r], r ? m->staging[r].p : m->shard[0].p, st[0]));
     if (m->transport == OM_TRANSPORT_RCCL && N > 1) {
@@ -486,8 +503,9 @@ om_status om_multi_render(om_multi* m, const om_camera* cam, const om_render_par
         if ((s = deal_frame(m, dev_frame, st))) return s;
         m->bound = dev_frame; m->bw = p->width; m->bh = p->height;
     } else if (m->ev0_live) {
-        // resident shards: the ranks start after rank 0's last deal or gather (which read them)
-        for (uint32_t r = 1; r < N; ++r) {
+        // resident shards: the ranks start after rank 0's last deal or gather (which read them);
+        // rank 0 too, as the caller may pass this render another stream than the gather's
+        for (uint32_t r = 0; r < N; ++r) {
             OM_MHIP(m, hipSetDevice(m->dev[r]));
             OM_MHIP(m, hipStreamWaitEvent(st[r], m->ev[0], 0));
         }
@@ -503,6 +521,7 @@ om_status om_multi_render(om_multi* m, const om_camera* cam, const om_render_par
         OM_MHIP(m, hipSetDevice(m->dev[r]));
         OM_MHIP(m, hipEventRecord(r ? m->ev[r] : m->done0, st[r]));
     }
+    m->renders_live = true;
     return OM_OK;
 }
 
@@ -547,7 +566,6 @@ om_status om_multi_gather(om_multi* m, om_pixel_stats* dev_frame, uint32_t W, ui
 void om_multi_reset(om_multi* m) {
     if (!m) return;
     m->bound = nullptr;
-    m->host_bound = nullptr;
 }
 
 om_status om_multi_render_host(om_multi* m, const om_camera* cam, const om_render_params* p, om_pixel_stats* stats,
@@ -562,17 +580,17 @@ om_status om_multi_render_host(om_multi* m, const om_camera* cam, const om_rende
         if (s != OM_OK) return merr(m, s, om_last_error(c));
     }
     OM_MHIP(m, hipSetDevice(m->dev[0]));
-    if (m->host_bound != stats || m->host_bytes != bytes) {
-        // a new host framebuffer: mirror it on devices[0] and deal it out (first call only)
-        m->host_bound = nullptr;
-        m->bound = nullptr;
-        OM_MHIP(m, m->host_frame.ensure(m->dev[0], bytes));
-        OM_MHIP(m, hipMemcpyAsync(m->host_frame.p, stats, bytes, hipMemcpyHostToDevice, st));
-        m->host_bound = stats; m->host_bytes = bytes;
-    }
+    // The host framebuffer is the caller's (render_thread.rs:145-147): it may have been zeroed to
+    // restart, rewritten, or freed and reallocated at the same address since the last call, so
+    // every call mirrors it on devices[0] and deals it out again.  This form is a
+    // synchronous round trip with two whole-frame copies anyway; om_multi_render keeps the
+    // shards resident across calls for device frames.
+    OM_MHIP(m, m->host_frame.ensure(m->dev[0], bytes));
+    m->bound = nullptr;
+    OM_MHIP(m, hipMemcpyAsync(m->host_frame.p, stats, bytes, hipMemcpyHostToDevice, st));
     om_status s = om_multi_render(m, cam, p, (om_pixel_stats*)m->host_frame.p, st);
     if (s == OM_OK) s = om_multi_gather(m, (om_pixel_stats*)m->host_frame.p, p->width, p->height, st);
-    if (s != OM_OK) { m->host_bound = nullptr; return s; }
+    if (s != OM_OK) return s;
     OM_MHIP(m, hipSetDevice(m->dev[0]));
     OM_MHIP(m, hipMemcpyAsync(stats, m->host_frame.p, bytes, hipMemcpyDeviceToHost, st));
     OM_MHIP(m, hipStreamSynchronize(st));

@@ -89,6 +89,12 @@ class Comm:
         with _stdout_to_stderr():
             check(lib.om_comm_init_rank(ctx, self.world_size, self.rank, idbuf, C.byref(self._c)), ctx)
 
+    def info(self):
+        """(nranks, rank) as RCCL reports them for this communicator (om_comm_info)."""
+        n, r = C.c_int32(), C.c_int32()
+        check(lib.om_comm_info(self._c, C.byref(n), C.byref(r)), self.ctx)
+        return n.value, r.value
+
     def render_shard(self, cam, params, dev_shard_ptr, stream=None):
         check(lib.om_render_shard(self._c, C.byref(cam.raw if hasattr(cam, "raw") else cam), C.byref(params),
                                   C.c_void_p(dev_shard_ptr), C.c_void_p(stream)), self.ctx)

@@ -188,3 +188,49 @@ def test_comm_rank_render_gather_scatter_through_rccl(om, oracle):
     assert nb == 0, msg
     comm.close()
     fz.close()
+
+
+def test_multi_redeal_without_gather(om):
+    """render(A) then render(B) with no gather between -- B's deal overwrites the
+    shards A's renders may still be writing, on another stream -- then gather(B) == one ctx."""
+    import torch
+    from raytracingoneweekend_amd import shard
+    W, H, spp, seed = W4K, H4K, 4, 46
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    ref = _full_frame(om, world, cam, W, H, 2, 1, seed, spp_total=spp)
+    mf = shard.MultiFrame([0, 0, 0], world)
+    a = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
+    b = torch.zeros_like(a)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    mf.render(cam, om.make_params(50, 0.001, 100.0, spp, W, H, sample_count=spp, seed=seed), a.data_ptr(), s1.cuda_stream)
+    mf.render(cam, om.make_params(50, 0.001, 100.0, spp, W, H, sample_count=2, seed=seed), b.data_ptr(), s2.cuda_stream)
+    mf.gather(b.data_ptr(), W, H, s2.cuda_stream)
+    torch.cuda.synchronize()
+    assert torch.equal(b, ref), f"{int((b != ref).view(-1, 40).any(1).sum())} pixels differ"
+    mf.close()
+
+
+def test_multi_render_host_sees_a_rewritten_buffer(om, oracle):
+    """the host form copies the caller's buffer on every call, so zeroing it restarts
+    the frame (no om_multi_reset needed) -- the same two calls give the same frame twice."""
+    import ctypes as C
+    from raytracingoneweekend_amd import _lib as L
+    from raytracingoneweekend_amd import shard
+    W, H, spp, seed = 160, 96, 3, 47
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    mf = shard.MultiFrame([0, 0], world)
+    buf = np.zeros(W * H, dtype=om.PIXEL_STATS_DTYPE)
+    p = om.make_params(50, 0.001, 100.0, spp, W, H, sample_count=spp, seed=seed)
+    mf._check(L.lib.om_multi_render_host(mf._m, C.byref(cam.raw), C.byref(p), buf.ctypes.data_as(C.c_void_p), None))
+    first = buf.copy()
+    assert (first["n"] == spp).all()
+    buf[:] = np.zeros(1, dtype=om.PIXEL_STATS_DTYPE)           # the caller restarts the frame in place
+    mf._check(L.lib.om_multi_render_host(mf._m, C.byref(cam.raw), C.byref(p), buf.ctypes.data_as(C.c_void_p), None))
+    assert np.array_equal(buf.view(np.uint8), first.view(np.uint8))
+    exp, _ = oracle.render(oracle.random_scene(0x5EED), oracle.default_camera(W / H), oracle.params(W, H, spp, seed=seed))
+    nb, msg = compare_stats(buf, exp, "render_host")
+    assert nb == 0, msg
+    mf.close()

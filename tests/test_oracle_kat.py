@@ -374,3 +374,18 @@ def test_oracle_nan_normal_scene_reaches_nan(om, oracle):
     st, _ = oracle.render(ow, oracle.default_camera(W / H), oracle.params(W, H, SPP, seed=31, march_steps=256))
     n_nan = int(np.isnan(st["sum"]).any(axis=1).sum())
     assert 0 < n_nan < W * H
+
+
+def test_threaded_pixel_windows_equal_single_thread_and_full_frame(oracle):
+    """oro_render_pixels_mt (the oracle windows of the full-size parity tests and bench.py) ==
+    the single-thread pixel-subset form == the same pixels of a whole-frame oro_render."""
+    W, H, spp = 40, 24, 5
+    w, cam = oracle.random_scene(0x5EED), oracle.default_camera(W / H)
+    p = oracle.params(W, H, spp, seed=9, max_depth=20)
+    pix = oracle.window_pixels(W, H, 7, 5, 12)
+    one = oracle.render_pixels(w, cam, p, pix)
+    mt = oracle.render_pixels(w, cam, p, pix, nthreads=3)
+    full, _ = oracle.render(w, cam, p)
+    assert np.array_equal(one.view(np.uint8), mt.view(np.uint8))
+    assert np.array_equal(one.view(np.uint8), full[pix].view(np.uint8))
+    assert pix[0] == 5 * W + 7 and pix[-1] == 16 * W + 18
