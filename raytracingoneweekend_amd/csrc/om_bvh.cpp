@@ -151,6 +151,28 @@ struct Builder {
     }
 };
 
+// IEEE half bits -> the value, exactly (every half is a float).
+float half_value(uint16_t h) {
+    const int e = (h >> 10) & 31, m = h & 1023;
+    const float v = e == 0 ? std::ldexp((float)m, -24) : e == 31 ? INFINITY : std::ldexp((float)(1024 + m), e - 25);
+    return (h & 0x8000u) ? -v : v;
+}
+
+// The half-precision plane that contains x on the outside: the largest half <= x (up = false, a
+// box's lo) or the smallest half >= x (up = true, its hi); +-inf beyond the half range.  Binary
+// search over the halves in value order (key k >= 0: bits k; k < 0: the negative half -k).
+uint16_t half_out(float x, bool up) {
+    auto bits = [](int k) { return (uint16_t)(k >= 0 ? k : (0x8000 | -k)); };
+    if (std::isnan(x)) return bits(up ? 0x7C00 : -0x7C00);
+    int lo = -0x7C00, hi = 0x7C00;                       // -inf .. +inf
+    if (!up) {                                           // largest k with value(k) <= x
+        while (lo < hi) { const int mid = lo + (hi - lo + 1) / 2; if (half_value(bits(mid)) <= x) lo = mid; else hi = mid - 1; }
+        return bits(lo);
+    }
+    while (lo < hi) { const int mid = lo + (hi - lo) / 2; if (half_value(bits(mid)) >= x) hi = mid; else lo = mid + 1; }
+    return bits(lo);
+}
+
 }  // namespace
 
 void build_bvh(const om_world& w, FrozenWorld& fw) {
@@ -263,7 +285,7 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     // compressed BVH2: both child boxes in the parent (one 64-B read per visit), emitted
     // breadth-first so the top levels, which every ray visits, are the first nodes: a tree
     // too big for LDS stages that prefix there (om_wavefront.hip, OM_WF_HYB_BYTES).
-    // direct leaf codes (OM_B2_DIRECT): when every record index fits 11 bits and every leaf holds
+    // direct leaf codes: when every record index fits 11 bits and every leaf holds
     // at most 15 records (S-traced: 485 records, leaves <= 8), a leaf child's 16-bit code is
     // OM_LEAF | first << 4 | count, so the traversal needs no leaf-table read to enter a leaf;
     // the table is still emitted (same order) for the other consumers.
@@ -272,7 +294,7 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     int32_t max_leaf = 0;
     for (const OmBvhNode& n : b.nodes)
         if (n.left < 0) max_leaf = std::max(max_leaf, n.right);
-    const bool direct = OM_B2_DIRECT && fw.srecs.size() < 2048u && max_leaf <= 15;
+    const bool direct = fw.srecs.size() < 2048u && max_leaf <= 15;
     struct Emit2 {
         const Builder& b; const std::vector<uint32_t>& leaf_first; std::vector<OmBvh2Node>& out;
         std::vector<uint32_t>& leaves;
@@ -325,6 +347,16 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
         e2.rec(root);
     }
     fw.b2_direct = direct ? 1u : 0u;
+    fw.b2h.clear();
+    for (const OmBvh2Node& n : fw.b2nodes) {
+        OmBvh2NodeH h{};
+        for (int i = 0; i < 3; ++i) {
+            h.b[i] = half_out(OM_B2_LO(n, 0, i), false); h.b[3 + i] = half_out(OM_B2_HI(n, 0, i), true);
+            h.b[6 + i] = half_out(OM_B2_LO(n, 1, i), false); h.b[9 + i] = half_out(OM_B2_HI(n, 1, i), true);
+        }
+        h.c0 = (uint16_t)n.c0; h.c1 = (uint16_t)n.c1; h.pad = 0u;
+        fw.b2h.push_back(h);
+    }
     // depth of the compressed tree (the traversal's stack bound)
     std::vector<uint32_t> depth(fw.b2nodes.size(), 1);
     fw.b2_depth = 1;

@@ -22,37 +22,13 @@ __device__ __forceinline__ F3 mul(F3 a, F3 b) { return f3(a.x * b.x, a.y * b.y, 
 __device__ __forceinline__ F3 scl(F3 a, float s) { return f3(a.x * s, a.y * s, a.z * s); }       // vec3.rs:220-235
 __device__ __forceinline__ F3 neg(F3 a) { return f3(-a.x, -a.y, -a.z); }
 __device__ __forceinline__ float dot(F3 a, F3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }    // vec3.rs:29-31
-// Square roots of the march SDFs.  hipcc's correctly rounded f32 sqrt is v_sqrt_f32 (<= 1 ulp)
-// plus a +-1-ulp correction, wrapped in range handling: inputs below 2^-96 are scaled by 2^32
-// (and the root by 2^-16), and +-0 / +inf pass through a class test.  For x >= 2^-96 (and
-// +inf) the wrapper selects nothing, so when every lane of the wave is in that range
-// (OM_MARCH_SQRT_CORE) the core alone runs: the same v_sqrt_f32, the same two fma residuals
-// and selects, hence the same bits, and ~7 fewer VALU (+2 s_nop) per root.  Otherwise the
-// whole wave takes sqrtf.  NaN inputs (never in range) always take sqrtf.
-#ifndef OM_MARCH_SQRT_CORE
-#define OM_MARCH_SQRT_CORE 0
-#endif
-__device__ __forceinline__ float sqrt_cr_core(float x) {
-    const float s = __builtin_amdgcn_sqrtf(x);
-    const float sm = __uint_as_float(__float_as_uint(s) - 1u), sp = __uint_as_float(__float_as_uint(s) + 1u);
-    float r = __builtin_fmaf(-sm, s, x) <= 0.0f ? sm : s;
-    r = __builtin_fmaf(-sp, s, x) > 0.0f ? sp : r;
-    return r;
-}
-template <bool CORE>
-__device__ __forceinline__ float sqrt_w(float x) {
-    if constexpr (CORE) {
-        if (__ballot(!(x >= 0x1p-96f)) == 0) return sqrt_cr_core(x);
-    }
-    return sqrtf(x);
-}
-__device__ __forceinline__ float march_sqrt(float x) { return sqrt_w<OM_MARCH_SQRT_CORE != 0>(x); }
-// OM_SQRT_CORE: the same for unit() and the sphere tests' discriminant roots (measured, off)
-#ifndef OM_SQRT_CORE
-#define OM_SQRT_CORE 0
-#endif
+// Square roots of the march SDFs: hipcc's correctly rounded f32 sqrt (v_sqrt_f32 plus a
+// +-1-ulp correction and its range handling).  A bare-core variant (range test skipped when a
+// whole wave is in range) was bit-exact but neutral on C2 and -13% on C1 in unit() (a uniform
+// branch in the divergent leaf loop), so sqrtf stays.
+__device__ __forceinline__ float march_sqrt(float x) { return sqrtf(x); }
 __device__ __forceinline__ F3 unit(F3 a) {                                                        // vec3.rs:35-40, 236-240
-    const float len = sqrt_w<OM_SQRT_CORE != 0>(dot(a, a));
+    const float len = sqrtf(dot(a, a));
     return scl(a, 1.0f / len);
 }
 __device__ __forceinline__ F3 at(F3 o, F3 d, float t) { return add(o, scl(d, t)); }              // ray.rs:14-16 (t*dir == dir*t)
@@ -105,12 +81,9 @@ __device__ __forceinline__ F3 rand_in_unit_sphere(Rng& g) {                     
 }
 
 // ---------------------------------------------------------------- traced.rs
-#ifndef OM_SPHERE_FAST_REJECT
-#define OM_SPHERE_FAST_REJECT 0
-#endif
 // Sphere::hit (traced.rs:39-62) up to the accepted root, from the ray in local space.
-// FASTREJ: the division-free rejection below regardless of OM_SPHERE_FAST_REJECT (bounce 0's
-// tile lists, OM_TILES_FAST_REJECT: coherent waves often reject an occluded candidate together).
+// FASTREJ: the division-free rejection below (bounce 0's tile lists: coherent waves often reject
+// an occluded candidate together; in the later bounces' divergent leaf loop it measured -0.4%).
 template <bool FASTREJ = false>
 __device__ __forceinline__ bool sphere_root_local(F3 lo, F3 ld, float tmin, float tmax, float& root) {
     const float a = dot(ld, ld);
@@ -118,9 +91,9 @@ __device__ __forceinline__ bool sphere_root_local(F3 lo, F3 ld, float tmin, floa
     const float c = dot(lo, lo) - 1.0f;
     const float disc = half_b * half_b - a * c;
     if (disc < 0.0f) return false;
-    const float sqrtd = sqrt_w<OM_SQRT_CORE != 0>(disc);
+    const float sqrtd = sqrtf(disc);
     const float n1 = -half_b - sqrtd, n2 = -half_b + sqrtd;
-    if (OM_SPHERE_FAST_REJECT || FASTREJ) {
+    if (FASTREJ) {
     // Both roots provably outside [tmin, tmax] without the two correctly rounded divisions
     // (~24 VALU): for a > 0 in the normal range, n < (tmin*a)(1-2^-18) implies
     // fl(n/a) < tmin and n > (tmax*a)(1+2^-18) implies fl(n/a) > tmax, whatever the f32
@@ -144,35 +117,6 @@ __device__ __forceinline__ bool sphere_root_local(F3 lo, F3 ld, float tmin, floa
 template <bool FASTREJ = false>
 __device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root) {
     return sphere_root_local<FASTREJ>(xform_p(T.w2l, o), xform_v(T.w2l, T.dz, d), tmin, tmax, root);
-}
-// Sphere::hit split in two (bounce 0's paired tile tests, om_trace.h): the expensive part (the
-// transform, the quadratic, sqrt and both quotients) does not depend on tmax, only the root
-// choice does, so two candidates' expensive parts can run interleaved and their choices in
-// order.  n2 / a is computed even when the near root is accepted (the reference skips it);
-// each quotient is the same IEEE operation, so the accepted root is bit-identical.
-struct SpherePre { float r1, r2; bool ok; };
-__device__ __forceinline__ SpherePre sphere_pre(const OmAffineTest& T, F3 o, F3 d) {
-    const F3 lo = xform_p(T.w2l, o), ld = xform_v(T.w2l, T.dz, d);
-    const float a = dot(ld, ld);
-    const float half_b = dot(lo, ld);
-    const float c = dot(lo, lo) - 1.0f;
-    const float disc = half_b * half_b - a * c;
-    SpherePre p;
-    p.ok = !(disc < 0.0f);
-    const float sqrtd = sqrt_w<OM_SQRT_CORE != 0>(disc);
-    p.r1 = (-half_b - sqrtd) / a;
-    p.r2 = (-half_b + sqrtd) / a;
-    return p;
-}
-__device__ __forceinline__ bool sphere_pick(const SpherePre& p, float tmin, float tmax, float& root) {
-    if (!p.ok) return false;
-    float r = p.r1;
-    if (r < tmin || r > tmax) {
-        r = p.r2;
-        if (r < tmin || r > tmax) return false;
-    }
-    root = r;
-    return true;
 }
 // The same test for a sphere whose world-to-local block is diagonal (off-diagonal entries
 // exactly +-0: an axis-aligned scaled sphere such as random_scene's ground, main.rs:38-40).
@@ -329,14 +273,10 @@ __device__ __forceinline__ float reflectance(float c, float ref_idx) {          
 }
 // Material::scatter (materials.rs:39-95); returns the unnormalised new direction
 // (Ray::new normalises it, ray.rs:11-13) and the attenuation.
-// OM_SCATTER_SHARED_SPHERE (default 1): Lambertian and Metal both draw one rand_in_unit_sphere
-// before anything else that consumes the stream (reflect draws nothing), so a wave holding both
-// kinds runs ONE rejection loop for them instead of one per kind; each path's draws are unchanged.
-#ifndef OM_SCATTER_SHARED_SPHERE
-#define OM_SCATTER_SHARED_SPHERE 1
-#endif
+// Lambertian and Metal both draw one rand_in_unit_sphere before anything else that consumes the
+// stream (reflect draws nothing), so a wave holding both kinds runs ONE rejection loop for them
+// instead of one per kind (C1 +2.4%); each path's draws are unchanged.
 __device__ __forceinline__ void scatter(const OmMaterial& m, F3 dir, F3 normal, Rng& g, F3& new_dir, F3& atten) {
-#if OM_SCATTER_SHARED_SPHERE
     if (m.type != 2) {
         const F3 r = rand_in_unit_sphere(g);                                                     // materials.rs:54 / :64
         if (m.type == 0) {                                                                       // lambertian :52-61
@@ -349,16 +289,6 @@ __device__ __forceinline__ void scatter(const OmMaterial& m, F3 dir, F3 normal, 
         }
         atten = ld3(m.albedo);
     } else {                                                                                     // dielectric :68-95
-#else
-    if (m.type == 0) {                                                                           // lambertian :52-61
-        F3 nd = add(normal, unit(rand_in_unit_sphere(g)));
-        if (fabsf(nd.x) < 1e-8f && fabsf(nd.y) < 1e-8f && fabsf(nd.z) < 1e-8f) nd = normal;      // near_zero vec3.rs:69-72
-        new_dir = nd; atten = ld3(m.albedo);
-    } else if (m.type == 1) {                                                                    // metal :62-66
-        const F3 refl = reflect(dir, normal);
-        new_dir = add(refl, scl(rand_in_unit_sphere(g), m.fuzz)); atten = ld3(m.albedo);
-    } else {                                                                                     // dielectric :68-95
-#endif
         const bool front = dot(dir, normal) < 0.0f;
         const float rr = front ? 1.0f / m.ior : m.ior;
         const F3 n = front ? normal : neg(normal);

@@ -127,24 +127,9 @@ struct OM_ALIGN16 OmAlwaysRec {
 // Compressed binary BVH node (64 B): both child boxes live in the parent, so one
 // node read yields both slab tests.  child = 16-bit code: node index, or
 // OM_LEAF | leaf index; b2leaves[leaf] = (first_record << 8) | count (records =
-// srecs, leaf order).  The traversal stack holds these 16-bit codes.
+// srecs, leaf order), or, when the records fit (om_bvh.cpp), the direct code
+// OM_LEAF | first << 4 | count.  The traversal stack holds these 16-bit codes.
 #define OM_LEAF 0x8000u
-#ifndef OM_B2_DIRECT
-#define OM_B2_DIRECT 1
-#endif
-// OM_PK_SLAB: the box planes interleaved as (lo, hi) pairs per axis, b[6k + 2i] = lo_k[i],
-// b[6k + 2i + 1] = hi_k[i], so one v_pk_fma_f32 gives both slab distances of an axis.
-#ifndef OM_PK_SLAB
-#define OM_PK_SLAB 0
-#endif
-#if OM_PK_SLAB
-struct OM_ALIGN16 OmBvh2Node {
-    float b[12];
-    uint32_t c0, c1, pad0, pad1;
-};
-#define OM_B2_LO(n, k, i) ((n).b[6 * (k) + 2 * (i)])
-#define OM_B2_HI(n, k, i) ((n).b[6 * (k) + 2 * (i) + 1])
-#else
 struct OM_ALIGN16 OmBvh2Node {
     float lo0[3];
     uint32_t c0;
@@ -157,7 +142,16 @@ struct OM_ALIGN16 OmBvh2Node {
 };
 #define OM_B2_LO(n, k, i) ((k) == 0 ? (n).lo0[i] : (n).lo1[i])
 #define OM_B2_HI(n, k, i) ((k) == 0 ? (n).hi0[i] : (n).hi1[i])
-#endif
+// The device form of the same node (32 B, r04): the child boxes as IEEE half-precision bits,
+// each plane rounded OUTWARD (lo down, hi up) from the f32 box, so a decoded box contains the
+// f32 one and the culling stays conservative (boxes only decide which exact tests run).  A visit
+// reads two 16-B words instead of four, and the slab test's fma takes the halves directly
+// (v_fma_mix_f32: no extra VALU).  b: child 0 lo xyz, hi xyz; child 1 lo xyz, hi xyz.
+struct OM_ALIGN16 OmBvh2NodeH {
+    uint16_t b[12];
+    uint16_t c0, c1;
+    uint32_t pad;
+};
 
 // Device view of a frozen world (passed by value as a kernel argument).
 struct OmSceneDev {
@@ -180,7 +174,7 @@ struct OmSceneDev {
     uint32_t n_snodes, n_srecs, n_always2;
     uint32_t lds_bytes;           // dynamic LDS the staged kernel needs (0 = scene too big: global path)
     // compressed BVH2 over the same leaves/records as the stackless BVH
-    const OmBvh2Node* b2nodes;
+    const OmBvh2NodeH* b2nodes;   // half-precision device nodes (om_bvh.cpp from FrozenWorld::b2nodes)
     const uint32_t* b2leaves;
     const OmAlwaysRec* always2_rec;  // always2 with boxes (BVH2 traversal)
     uint32_t n_b2nodes, n_b2leaves;

@@ -4,8 +4,14 @@
 #pragma once
 #include "om_device.h"
 #include "om_layout.h"
+#include "om_tuning.h"
 
 namespace omd {
+
+// BVH2 traversal: "no next node" (child codes are 16-bit)
+constexpr uint32_t kB2Done = 0x10000u;
+// A half-precision box plane (OmBvh2NodeH) as f32, exactly.
+__device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 
 // Slab-test min/max (kept as fminf/fmaxf: an inline-asm v_min/v_max variant that skips
 // LLVM's canonicalising v_max x,x of loop-carried operands measured 12% slower, because the
@@ -26,40 +32,19 @@ __device__ __forceinline__ float slab_far(float x0, float x1, float y0, float y1
 // the hardware reciprocal (1 ulp) instead of the correctly rounded division, ~10 VALU each.
 // Boxes are inflated by 1e-3*(1+extent) and the t window is loosened by 1e-4 relative, far
 // beyond its error; the component is kept >= 1e-20 in magnitude, so the result is finite.
-// OM_EXACT_INVDIR restores the division (timing ablation).
 __device__ __forceinline__ float inv_dir(float c) {
     const float k = fabsf(c) > 1e-20f ? c : copysignf(1e-20f, c);
-#ifdef OM_EXACT_INVDIR
-    return 1.0f / k;
-#else
     return __builtin_amdgcn_rcpf(k);
-#endif
 }
 
 // Work counters (om_counters); compiled out (COUNT=false) of the production kernels so
 // they cost no registers — the bench counts work in a separate, identical launch.
-// lap(k): the diagnostic build OM_PHASE_STAMPS=2 (tools/phase_stamps.py) splits the trace's
-// time into the steps below (every lap waits for outstanding memory first, so a lap after a
-// load measures that load's latency); a no-op otherwise.
-enum { LAP_ALWAYS2 = 0, LAP_NODE_WAIT, LAP_NODE_SLAB, LAP_POP, LAP_REC_WAIT, LAP_REC_TEST, LAP_N };
 template <bool COUNT>
 struct WorkT {
     uint32_t prim = 0, pre = 0, march = 0;
     __device__ __forceinline__ void add_prim() { if (COUNT) prim++; }
     __device__ __forceinline__ void add_pre(uint32_t k = 1) { if (COUNT) pre += k; }
     __device__ __forceinline__ void add_march() { if (COUNT) march++; }
-#if defined(OM_PHASE_STAMPS) && OM_PHASE_STAMPS == 2
-    uint64_t lt = 0, lacc[LAP_N] = {0, 0, 0, 0, 0, 0}, lcnt[LAP_N] = {0, 0, 0, 0, 0, 0};
-    __device__ __forceinline__ void lap_start() { __builtin_amdgcn_s_waitcnt(0); lt = __builtin_amdgcn_s_memtime(); }
-    __device__ __forceinline__ void lap(int k) {
-        __builtin_amdgcn_s_waitcnt(0);
-        const uint64_t n = __builtin_amdgcn_s_memtime();
-        lacc[k] += n - lt; lcnt[k] += 1; lt = n;
-    }
-#else
-    __device__ __forceinline__ void lap_start() {}
-    __device__ __forceinline__ void lap(int) {}
-#endif
 };
 
 // Exact test of global primitive gi with the brute-force acceptance (root <= tmax).
@@ -178,13 +163,9 @@ __device__ __forceinline__ int traced_bvh(const OmSceneDev& S, F3 o, F3 d, float
 // because the kernels' global stores may alias the scene arrays (they never do: the scene is
 // immutable while a kernel runs, om_upload_world happens between calls).  The always2 records
 // are read by every ray of every wave: through the vector path each one was a dependent L2
-// round trip queued behind the path-state streams.
-#ifndef OM_A2_SCALAR
-#define OM_A2_SCALAR 1
-#endif
+// round trip queued behind the path-state streams (C1 +3.1%).
 template <class T>
 __device__ __forceinline__ T uniform_load(const T* p) {
-#if OM_A2_SCALAR
     static_assert(sizeof(T) % 4 == 0, "dword records");
     typedef const __attribute__((address_space(4))) uint32_t cu32;
     cu32* q = (cu32*)p;
@@ -193,9 +174,6 @@ __device__ __forceinline__ T uniform_load(const T* p) {
 #pragma unroll
     for (uint32_t i = 0; i < sizeof(T) / 4; ++i) d[i] = q[i];
     return r;
-#else
-    return *p;
-#endif
 }
 
 // Exact test of global primitive gi (wave-uniform) with the reference's acceptance, the record
@@ -214,61 +192,27 @@ __device__ __forceinline__ void offer_uniform(const OmSceneDev& S, uint32_t gi, 
     if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
 }
 
-// The primitives outside the BVH trees (always2): conservative box first, then the
-// exact test with the brute-force tie rule.  OM_DIAG_SPHERE: an unbounded record flagged as
-// an axis-aligned sphere takes sphere_root_diag (same accepted root, 24 fewer VALU).
-#ifndef OM_DIAG_SPHERE
-#define OM_DIAG_SPHERE 1
-#endif
-// OM_A2_PRELOAD: with at most 4 always2 records (every reference scene), all of them are loaded
-// up front (their scalar loads in flight together) and the loop is unrolled, so each record's
-// test no longer starts with a dependent s_load round trip.
-#ifndef OM_A2_PRELOAD
-#define OM_A2_PRELOAD 0
-#endif
-template <class Wk>
-__device__ __forceinline__ void offer_always2_one(const OmSceneDev& S, const OmAlwaysRec& A, F3 o, F3 d, float tmin, float ix,
-                                                  float iy, float iz, float nox, float noy, float noz, float t_lo,
-                                                  float& closest, int& best, Wk& w);
+// The primitives outside the BVH trees (always2), in index order: conservative box first, then
+// the exact test with the brute-force tie rule.  An unbounded record (huge primitives, planes:
+// lo = -inf) passes every slab test, so it skips it (+0.6% on C1); one flagged as an
+// axis-aligned sphere (the ground) takes sphere_root_diag (same accepted root, 24 fewer VALU).
 template <class Wk>
 __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, float tmin, float ix, float iy, float iz,
                                               float nox, float noy, float noz, float t_lo, float& closest, int& best, Wk& w) {
-#if OM_A2_PRELOAD
-    if (S.n_always2 <= 4u) {
-        OmAlwaysRec A[4];
-#pragma unroll
-        for (uint32_t k = 0; k < 4u; ++k) if (k < S.n_always2) A[k] = uniform_load(S.always2_rec + k);
-#pragma unroll
-        for (uint32_t k = 0; k < 4u; ++k)
-            if (k < S.n_always2) offer_always2_one(S, A[k], o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
-        return;
-    }
-#endif
-    for (uint32_t k = 0; k < S.n_always2; ++k)
-        offer_always2_one(S, uniform_load(S.always2_rec + k), o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
-}
-template <class Wk>
-__device__ __forceinline__ void offer_always2_one(const OmSceneDev& S, const OmAlwaysRec& A, F3 o, F3 d, float tmin, float ix,
-                                                  float iy, float iz, float nox, float noy, float noz, float t_lo,
-                                                  float& closest, int& best, Wk& w) {
-    {
-#ifndef OM_ALWAYS2_INF_SLAB
-        // an unbounded record (huge primitives, planes: lo = -inf) passes every slab test
+    for (uint32_t k = 0; k < S.n_always2; ++k) {
+        const OmAlwaysRec A = uniform_load(S.always2_rec + k);
         if (A.lo[0] == -INFINITY) {
-#if OM_DIAG_SPHERE
-            if (A.pad == OM_ALWAYS_DIAG_SPHERE && tmin > 0.0f) {                // axis-aligned sphere (the ground)
+            if (A.pad == OM_ALWAYS_DIAG_SPHERE && tmin > 0.0f) {
                 float t;
                 w.add_prim();
                 if (sphere_root_diag(uniform_load(S.sph_test + A.gi), o, d, tmin, closest, t) && (t < closest || (int)A.gi > best)) {
                     closest = t; best = (int)A.gi;
                 }
-                return;
+            } else {
+                offer_uniform(S, A.gi, o, d, tmin, closest, best, w);
             }
-#endif
-            offer_uniform(S, A.gi, o, d, tmin, closest, best, w);
-            return;
+            continue;
         }
-#endif
         w.add_pre();
         const float t_hi = closest * 1.0001f + 1e-3f;
         const float x0 = __builtin_fmaf(A.lo[0], ix, nox), x1 = __builtin_fmaf(A.hi[0], ix, nox);
@@ -289,10 +233,8 @@ __device__ __forceinline__ void test_rec(const OmAffineTest& R, F3 o, F3 d, floa
     float t;
     int ax;
     w.add_prim();
-    w.lap(LAP_REC_WAIT);
     const bool h = (tag >> 31) ? cube_root(R, o, d, tmin, closest, t, ax) : sphere_root<FASTREJ>(R, o, d, tmin, closest, t);
     if (h && (t < closest || (int)gi > best)) { closest = t; best = (int)gi; }
-    w.lap(LAP_REC_TEST);
 }
 
 // (first record << 8) | count of the leaf with child code `code`: straight from a direct code
@@ -411,27 +353,10 @@ struct MTorusSdf {
         bc[0] = T.bc[0]; bc[1] = T.bc[1]; bc[2] = T.bc[2];
     }
 };
-template <uint32_t NS, uint32_t NB, uint32_t NT>
-struct MarchedExact {
-    static constexpr uint32_t KS = NS, KB = NB, KT = NT;      // for_objects: unrolled (0: no loop)
-    static constexpr bool INDEXED = false;
-    static constexpr bool RELOAD = false;
-    static constexpr uint32_t ns = NS, nb = NB, nt = NT;
-    OmMSphere s[NS ? NS : 1]; OmMBox b[NB ? NB : 1]; MTorusSdf t[NT ? NT : 1];
-    __device__ explicit MarchedExact(const OmSceneDev& S) {
-#pragma unroll
-        for (uint32_t i = 0; i < NS; ++i) s[i] = S.msph[i];
-#pragma unroll
-        for (uint32_t i = 0; i < NB; ++i) b[i] = S.mbox[i];
-#pragma unroll
-        for (uint32_t i = 0; i < NT; ++i) t[i].load(S.mtor[i]);
-    }
-    __host__ __device__ static bool matches(uint32_t n_s, uint32_t n_b, uint32_t n_t) { return n_s == NS && n_b == NB && n_t == NT; }
-};
-
-// The same exact-count view with the parameters staged in LDS (the north_star's "LDS-staged SDF
-// params"; OM_WF_MARCH_EXACT = 2 selects it for k_march): one workgroup-wide copy,
-// every step reads them with broadcast ds_reads at constant offsets.
+// An exact-count view: EXACTLY NS spheres, NB boxes and NT tori with only the fields the march
+// reads (a torus: 24 of its 43 floats, MTorusSdf), staged in LDS once per workgroup (the
+// north_star's "LDS-staged SDF params", k_march): fully unrolled steps with no
+// count guards, every step reads them with broadcast ds_reads at constant offsets.
 template <uint32_t NS, uint32_t NB, uint32_t NT>
 struct MarchedExactLds {
     static constexpr uint32_t KS = NS, KB = NB, KT = NT;
@@ -442,6 +367,7 @@ struct MarchedExactLds {
     static constexpr uint32_t ns = NS, nb = NB, nt = NT;
     struct Block { OmMSphere s[NS ? NS : 1]; OmMBox b[NB ? NB : 1]; MTorusSdf t[NT ? NT : 1]; };
     const OmMSphere* s; const OmMBox* b; const MTorusSdf* t;
+    __host__ __device__ static bool matches(uint32_t n_s, uint32_t n_b, uint32_t n_t) { return n_s == NS && n_b == NB && n_t == NT; }
     // every thread of the block calls it (it ends with a barrier)
     __device__ MarchedExactLds(const OmSceneDev& S, Block* lds) : s(lds->s), b(lds->b), t(lds->t) {
         const uint32_t i = threadIdx.x;
@@ -468,87 +394,9 @@ __device__ __forceinline__ void for_objects(uint32_t n, F body) {
 // (the first minimum wins; hits.rs:296-322, 341-358).  An object whose conservative lower
 // bound (om_world.cpp) proves |sdf| > best cannot be the new minimum and is skipped: the
 // result is bit-identical to evaluating every SDF.  -> best (INFINITY if none), kind, index.
-//
-// OM_MARCH_PREFETCH (arrays view, measured and off: C2 -7%): every object's
-// parameters are scalar loads that the loop's hit-buffer stores keep the compiler from
-// hoisting, so each object costs a load round trip (s_load + s_waitcnt) before its SDF.  The
-// pipelined form issues the first sphere, box and torus-cull loads together at the top of the
-// step and each type's next object before the current one's SDF (clamped index: always in
-// range, no branch); same objects, same order, same arithmetic.  Empty types read a zero
-// dummy object that no loop iteration uses.
-#ifndef OM_MARCH_PREFETCH
-#define OM_MARCH_PREFETCH 0
-#endif
-static __device__ const OmMSphere kNoMSphere = {};
-static __device__ const OmMBox kNoMBox = {};
-static __device__ const OmMTorus kNoMTorus = {};
-// Loads through the constant address space: always scalar (s_load), whatever the loop stores,
-// so the next object's parameters can be in flight while the current SDF runs.  The scene
-// arrays are immutable while a kernel runs (om_upload_world between calls only).
-typedef const __attribute__((address_space(4))) float om_cfloat;
-__device__ __forceinline__ om_cfloat* cptr(const void* q) { return (om_cfloat*)q; }
-struct SphereP { float x, y, z, r; };
-struct BoxP { float cx, cy, cz, sx, sy, sz, br; };
-struct TorusCull { float x, y, z, bk, br; };
-__device__ __forceinline__ SphereP load_sphere(const OmMSphere* q) {
-    om_cfloat* f = cptr(q);
-    return SphereP{f[0], f[1], f[2], f[3]};
-}
-__device__ __forceinline__ BoxP load_box(const OmMBox* q) {
-    om_cfloat* f = cptr(q);
-    return BoxP{f[0], f[1], f[2], f[4], f[5], f[6], f[7]};
-}
-__device__ __forceinline__ TorusCull load_torus_cull(const OmMTorus* q) {
-    om_cfloat* f = cptr(q->bc);
-    return TorusCull{f[0], f[1], f[2], f[3], f[4]};
-}
-
-__device__ __forceinline__ float nearest_marched_pf(const MarchedArrays& m, F3 p, int& bk, uint32_t& bi) {
-    float best = INFINITY;
-    bk = -1; bi = 0;
-    const OmMSphere* S = m.ns ? m.s : &kNoMSphere;
-    const OmMBox* B = m.nb ? m.b : &kNoMBox;
-    const OmMTorus* T = m.nt ? m.t : &kNoMTorus;
-    SphereP sc = load_sphere(S);
-    BoxP bc = load_box(B);
-    TorusCull tc = load_torus_cull(T);
-    for (uint32_t i = 0; i < m.ns; ++i) {
-        const SphereP sn = load_sphere(S + (i + 1u < m.ns ? i + 1u : i));
-        OmMSphere Q;
-        Q.center[0] = sc.x; Q.center[1] = sc.y; Q.center[2] = sc.z; Q.radius = sc.r;
-        const float v = fabsf(msphere_sdf(Q, p));
-        if (v < best) { best = v; bk = 0; bi = i; }
-        sc = sn;
-    }
-    for (uint32_t i = 0; i < m.nb; ++i) {
-        const BoxP bn = load_box(B + (i + 1u < m.nb ? i + 1u : i));
-        const float dx = p.x - bc.cx, dy = p.y - bc.cy, dz = p.z - bc.cz;
-        const float thr = (best + bc.br) * 1.0001f;                            // inf/NaN -> evaluate
-        if (!(dx * dx + dy * dy + dz * dz > thr * thr)) {
-            OmMBox Q;
-            Q.center[0] = bc.cx; Q.center[1] = bc.cy; Q.center[2] = bc.cz; Q.pad0 = 0.0f;
-            Q.sizes[0] = bc.sx; Q.sizes[1] = bc.sy; Q.sizes[2] = bc.sz; Q.br = bc.br;
-            const float v = fabsf(mbox_sdf(Q, p));
-            if (v < best) { best = v; bk = 1; bi = i; }
-        }
-        bc = bn;
-    }
-    for (uint32_t i = 0; i < m.nt; ++i) {
-        const TorusCull tn = load_torus_cull(T + (i + 1u < m.nt ? i + 1u : i));
-        const float dx = p.x - tc.x, dy = p.y - tc.y, dz = p.z - tc.z;
-        const float thr = best * tc.bk + tc.br;                                // inf/NaN -> evaluate
-        if (!(dx * dx + dy * dy + dz * dz > thr * thr)) {
-            const float v = fabsf(mtorus_sdf(T[i], p));
-            if (v < best) { best = v; bk = 2; bi = i; }
-        }
-        tc = tn;
-    }
-    return best;
-}
 
 template <class M>
 __device__ __forceinline__ float nearest_marched(const M& m, F3 p, int& bk, uint32_t& bi) {
-    if constexpr (OM_MARCH_PREFETCH && M::INDEXED) return nearest_marched_pf(m, p, bk, bi);
     if constexpr (M::RELOAD) __atomic_signal_fence(__ATOMIC_SEQ_CST);
     float best = INFINITY;
     bk = -1; bi = 0;
@@ -610,60 +458,15 @@ __device__ __forceinline__ bool march_begin(const M& m, F3 o, F3 d, float tmin, 
     return true;
 }
 
-// Escape test: true when no point the march can still visit lies within HIT
-// of a marched object, so the march ends without a hit whatever its remaining steps do —
-// and a miss's result does not depend on t or on how many steps ran (hits.rs:294-332: the
-// traced `closest`/winner stand).  Per object: a centre c and a radius rho such that every
-// computed point with |p - c| > rho has computed |sdf| > HIT (sphere: (r + HIT)(1 + 1e-5) +
-// 1e-5 covers the <= 4u error of |p - c| - r; box and torus: their march-cull bounds with
-// best = HIT).  The march's future points lie within e_p <= 4u(|o|_1 + T) of the half-line
-// {p + d s, s >= 0}, T = min(tmax, closest) > t (hits.rs:294), so it suffices that the
-// half-line's closest approach to c, sqrt(|w|^2 - min(d.w, 0)^2) with w = p - c, exceeds
-// rho + 2e-6(|o|_1 + T) (2.5x the two e_p), after a 1e-5 |w|^2 allowance for the f32
-// evaluation of the squared approach (<= 12u |w|^2).  Infinite T, NaN or inf anywhere:
-// false.  The test never touches output bits, so it may round freely within those margins.
-#ifndef OM_MARCH_ESCAPE
-#define OM_MARCH_ESCAPE 0
-#endif
-template <class M>
-__device__ __forceinline__ bool march_escapes(const M& m, F3 o, F3 d, F3 p, float T) {
-    const float HIT = 0.001f;
-    const float E = 2e-6f * (((fabsf(o.x) + fabsf(o.y)) + fabsf(o.z)) + T);
-    bool esc = true;
-    auto clear = [&](float cx, float cy, float cz, float rho) {
-        const float wx = p.x - cx, wy = p.y - cy, wz = p.z - cz;
-        const float ww = wx * wx + wy * wy + wz * wz;
-        const float pm = fminf(d.x * wx + d.y * wy + d.z * wz, 0.0f);
-        const float a = rho + E;
-        esc = esc && (ww - pm * pm) - 1e-5f * ww > a * a;
-    };
-    for_objects<M::KS>(m.ns, [&](uint32_t i) {
-        const OmMSphere& Q = m.s[i];
-        clear(Q.center[0], Q.center[1], Q.center[2], (Q.radius + HIT) * 1.00001f + 1e-5f);
-    });
-    for_objects<M::KB>(m.nb, [&](uint32_t i) {
-        const OmMBox& B = m.b[i];
-        clear(B.center[0], B.center[1], B.center[2], (HIT + B.br) * 1.0001f);
-    });
-    for_objects<M::KT>(m.nt, [&](uint32_t i) {
-        const auto& Q = m.t[i];
-        clear(Q.bc[0], Q.bc[1], Q.bc[2], HIT * Q.bk + Q.br);
-    });
-    return esc;
-}
-
 // One iteration of the sphere-tracing loop (hits.rs:294-332).  Returns 0 to continue, 1 on
 // a hit (gi = the marched winner's global index, the hit is at t), 2 when the march ends
-// without one.  Every 4th step first runs the escape test above (2: the same miss, sooner).
+// without one.
 template <class M, class Wk>
 __device__ __forceinline__ int march_step(const OmSceneDev& S, const M& m, F3 o, F3 d, float tmax, float closest, float& t,
                                           uint32_t& iters, int& gi, Wk& w) {
     const float HIT = 0.001f;
     if (!(t < tmax && t < closest && iters > 0)) return 2;                    // hits.rs:294
     const F3 p = at(o, d, t);
-#if OM_MARCH_ESCAPE
-    if ((iters & 3u) == 0u && march_escapes(m, o, d, p, fminf(tmax, closest))) return 2;
-#endif
     iters -= 1;
     w.add_march();
     int bk;
@@ -696,9 +499,7 @@ __device__ __forceinline__ int march_with(const OmSceneDev& S, const M& m, F3 o,
 template <class Wk>
 __device__ __forceinline__ int march(const OmSceneDev& S, F3 o, F3 d, float tmin, float tmax, float closest,
                                      uint32_t steps, float& t_hit, Wk& w) {
-#ifndef OM_MARCH_ARRAYS_ONLY
     if (MarchedSmall::fits(S)) return march_with(S, MarchedSmall(S), o, d, tmin, tmax, closest, steps, t_hit, w);
-#endif
     return march_with(S, MarchedArrays(S), o, d, tmin, tmax, closest, steps, t_hit, w);
 }
 
@@ -801,22 +602,14 @@ __device__ __forceinline__ int nonfinite_hit(const OmSceneDev& S, float& closest
 // Primary ray with a per-tile candidate list (om_tiles.h): always2, then
 // every record the conservative lens-aware frustum of its 8x8 tile can reach — the
 // brute-force loop of hits.rs:274-285 over a superset of the records it could accept.
-#ifndef OM_TILES_FAST_REJECT
-#define OM_TILES_FAST_REJECT 1
-#endif
-#ifndef OM_TILES_PAIRED
-#define OM_TILES_PAIRED 0      // measured: -0.4% on C1
-#endif
 // UNIFORM: every lane of the wave is in tile `tile` (the caller checked it; a bounce-0 wave is one
 // 8x8 tile of one sample except where partial tiles meet), so the list and its records are read
 // with scalar loads (uniform_load) instead of vector loads.
 // tnear (UNIFORM): the lists are sorted by a lower bound of the t at which any primary ray can
 // reach the record's box (om_tiles.cpp); once every lane's closest is below the next record's
 // bound, that record and all later ones would be rejected (root >= bound > closest = tmax), so
-// the wave stops (OM_TILES_EARLY_OUT).  NaN closest keeps testing.
-#ifndef OM_TILES_EARLY_OUT
-#define OM_TILES_EARLY_OUT 1
-#endif
+// the wave stops (C1 +0.6%).  NaN closest keeps testing.  The candidates take sphere_root's
+// division-free rejection (FASTREJ): coherent waves often reject an occluded candidate together.
 template <bool UNIFORM = false, class Wk>
 __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t* toff, const uint16_t* tidx, uint32_t tile,
                                             F3 o, F3 d, float tmin, float& closest, Wk& w, const float* tnear = nullptr) {
@@ -835,32 +628,10 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
             return (k & 1u) ? pair >> 16 : pair & 0xFFFFu;
         };
         uint32_t k = b;
-#if OM_TILES_PAIRED
-        // two sphere candidates at a time: their tmax-independent parts interleaved (two
-        // dependency chains in flight: bounce 0 stalls on issue, not memory), the root choices
-        // and the acceptances in list order (each with the closest the previous one left)
-        for (; k + 1u < e; k += 2u) {
-            const OmAffineTest R0 = uniform_load(S.srecs + rec_at(k)), R1 = uniform_load(S.srecs + rec_at(k + 1u));
-            uint32_t t0, t1;
-            __builtin_memcpy(&t0, &R0.pad, 4);
-            __builtin_memcpy(&t1, &R1.pad, 4);
-            if ((t0 | t1) >> 31) {                                   // a cube: the plain tests
-                test_rec(R0, o, d, tmin, closest, best, w);
-                test_rec(R1, o, d, tmin, closest, best, w);
-                continue;
-            }
-            const SpherePre p0 = sphere_pre(R0, o, d), p1 = sphere_pre(R1, o, d);
-            float t;
-            w.add_prim();
-            if (sphere_pick(p0, tmin, closest, t) && (t < closest || (int)t0 > best)) { closest = t; best = (int)t0; }
-            w.add_prim();
-            if (sphere_pick(p1, tmin, closest, t) && (t < closest || (int)t1 > best)) { closest = t; best = (int)t1; }
-        }
-#endif
         for (; k < e; ++k) {
             const uint32_t r = rec_at(k);
-            if (OM_TILES_EARLY_OUT && tnear && __ballot(!(closest < uniform_load(tnear + r))) == 0) break;
-            test_rec<OM_TILES_FAST_REJECT>(uniform_load(S.srecs + r), o, d, tmin, closest, best, w);
+            if (tnear && __ballot(!(closest < uniform_load(tnear + r))) == 0) break;
+            test_rec<true>(uniform_load(S.srecs + r), o, d, tmin, closest, best, w);
         }
     } else {
         const uint32_t e = toff[tile + 1];
@@ -871,14 +642,11 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
 
 // HYB: only nodes [0, nl) are in `nodes` (the breadth-first prefix staged in LDS); the
 // others are read from `gnodes` (global memory, through L2).
-#ifndef OM_B2_TOS
-#define OM_B2_TOS 0
-#endif
 template <int DEPTH, int STRIDE, class Wk, bool HYB = false>
-__device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node* nodes, const uint32_t* leaves,
+__device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2NodeH* nodes, const uint32_t* leaves,
                                            const OmAffineTest* recs, uint16_t* stk,
                                            F3 o, F3 d, float tmin, float& closest, Wk& w,
-                                           const OmBvh2Node* gnodes = nullptr, uint32_t nl = 0) {
+                                           const OmBvh2NodeH* gnodes = nullptr, uint32_t nl = 0) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
     const float ix = inv_dir(d.x);
@@ -886,199 +654,72 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
     const float iz = inv_dir(d.z);
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
-    w.lap_start();
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
-    w.lap(LAP_ALWAYS2);
-    uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
+    // one node visit: -> the next code (near child, the only hit child, or a pop; kB2Done when
+    // the stack is empty), the far child pushed.  The stack needs one entry per internal level
+    // on the current path (om_upload_world enables the BVH2 only when its depth <= DEPTH).
     int sp = 0;
-    bool overflow = false;
-#if OM_B2_TOS
-    // the stack's top entry lives in a register: a pop takes it at once and re-reads the next
-    // one from LDS off the critical path (needed only at the next pop); LDS holds sp - 1 entries
-    uint32_t tos = 0;
-#define OM_B2_POP()                                                   \
-    do {                                                              \
-        cur = tos; --sp;                                              \
-        if (sp > 0) tos = stk[(sp - 1) * STRIDE];                     \
-    } while (0)
-#define OM_B2_PUSH(c)                                                 \
-    do {                                                              \
-        if (sp > 0) stk[(sp - 1) * STRIDE] = (uint16_t)tos;           \
-        tos = (c); ++sp;                                              \
-    } while (0)
-#else
-#define OM_B2_POP() do { --sp; cur = stk[sp * STRIDE]; } while (0)
-#define OM_B2_PUSH(c) do { stk[sp * STRIDE] = (uint16_t)(c); ++sp; } while (0)
-#endif
-    for (;;) {
-        if (cur & OM_LEAF) {                            // the single leaf site
-            test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
-            if (sp == 0) break;
-            OM_B2_POP();
-            w.lap(LAP_POP);
-            continue;
-        }
-        const OmBvh2Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
-        w.lap(LAP_NODE_WAIT);
+    auto pop = [&]() -> uint32_t {
+        if (sp == 0) return kB2Done;
+        --sp;
+        return stk[sp * STRIDE];
+    };
+    auto visit = [&](uint32_t node) -> uint32_t {
+        const OmBvh2NodeH N = (HYB && node >= nl) ? gnodes[node] : nodes[node];
         w.add_pre(2);
         const float t_hi = closest * 1.0001f + 1e-3f;
-#if OM_PK_SLAB
-        // (lo, hi) plane pairs: one v_pk_fma_f32 per axis and box (same fma per lane)
-        typedef float pkf2 __attribute__((ext_vector_type(2)));
-        const pkf2* B = (const pkf2*)N.b;
-        const pkf2 IX = {ix, ix}, IY = {iy, iy}, IZ = {iz, iz}, OX = {nox, nox}, OY = {noy, noy}, OZ = {noz, noz};
-        pkf2 X = __builtin_elementwise_fma(B[0], IX, OX), Y = __builtin_elementwise_fma(B[1], IY, OY),
-             Z = __builtin_elementwise_fma(B[2], IZ, OZ);
-        const float n0 = slab_near(X.x, X.y, Y.x, Y.y, Z.x, Z.y, t_lo);
-        const float f0 = slab_far(X.x, X.y, Y.x, Y.y, Z.x, Z.y, t_hi);
-        X = __builtin_elementwise_fma(B[3], IX, OX); Y = __builtin_elementwise_fma(B[4], IY, OY);
-        Z = __builtin_elementwise_fma(B[5], IZ, OZ);
-        const float n1 = slab_near(X.x, X.y, Y.x, Y.y, Z.x, Z.y, t_lo);
-        const float f1 = slab_far(X.x, X.y, Y.x, Y.y, Z.x, Z.y, t_hi);
-#else
-        float x0 = __builtin_fmaf(N.lo0[0], ix, nox), x1 = __builtin_fmaf(N.hi0[0], ix, nox);
-        float y0 = __builtin_fmaf(N.lo0[1], iy, noy), y1 = __builtin_fmaf(N.hi0[1], iy, noy);
-        float z0 = __builtin_fmaf(N.lo0[2], iz, noz), z1 = __builtin_fmaf(N.hi0[2], iz, noz);
+        // (float)half operands: the fma becomes v_fma_mix_f32 (the conversion is free)
+        float x0 = __builtin_fmaf(h2f(N.b[0]), ix, nox), x1 = __builtin_fmaf(h2f(N.b[3]), ix, nox);
+        float y0 = __builtin_fmaf(h2f(N.b[1]), iy, noy), y1 = __builtin_fmaf(h2f(N.b[4]), iy, noy);
+        float z0 = __builtin_fmaf(h2f(N.b[2]), iz, noz), z1 = __builtin_fmaf(h2f(N.b[5]), iz, noz);
         const float n0 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
         const float f0 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
-        x0 = __builtin_fmaf(N.lo1[0], ix, nox); x1 = __builtin_fmaf(N.hi1[0], ix, nox);
-        y0 = __builtin_fmaf(N.lo1[1], iy, noy); y1 = __builtin_fmaf(N.hi1[1], iy, noy);
-        z0 = __builtin_fmaf(N.lo1[2], iz, noz); z1 = __builtin_fmaf(N.hi1[2], iz, noz);
+        x0 = __builtin_fmaf(h2f(N.b[6]), ix, nox); x1 = __builtin_fmaf(h2f(N.b[9]), ix, nox);
+        y0 = __builtin_fmaf(h2f(N.b[7]), iy, noy); y1 = __builtin_fmaf(h2f(N.b[10]), iy, noy);
+        z0 = __builtin_fmaf(h2f(N.b[8]), iz, noz); z1 = __builtin_fmaf(h2f(N.b[11]), iz, noz);
         const float n1 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
         const float f1 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
-#endif
         const bool h0 = !(n0 > f0), h1 = !(n1 > f1);
         if (h0 && h1) {                                 // near child next, far child pushed
             const bool swap = n1 < n0;
-            const uint32_t nearc = swap ? N.c1 : N.c0, farc = swap ? N.c0 : N.c1;
-            if (sp < DEPTH) OM_B2_PUSH(farc);
-            else overflow = true;
-            cur = nearc;
-        } else if (h0 || h1) {
-            cur = h0 ? N.c0 : N.c1;
-        } else {
-            w.lap(LAP_NODE_SLAB);
-            if (sp == 0) break;
-            OM_B2_POP();
-            w.lap(LAP_POP);
-            continue;
+            if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1); ++sp; }
+            return swap ? N.c1 : N.c0;
         }
-        w.lap(LAP_NODE_SLAB);
+        if (h0 || h1) return h0 ? N.c0 : N.c1;
+        return pop();
+    };
+    uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
+    if constexpr (OM_B2_SPECULATIVE) {
+        // speculative while-while (Aila & Laine 2009): the node loop runs until every lane of the
+        // wave holds a leaf; a lane that reaches its first leaf postpones it and keeps descending
+        // (a second leaf stops it).  Then the lanes test their leaves together.  The winner does
+        // not depend on the order of the tests (the tie rule above), so the result is the same.
+        uint32_t leaf = 0;                              // postponed leaf code (OM_LEAF set), 0 = none
+        while (cur != kB2Done || leaf) {
+            while (cur != kB2Done && !(cur & OM_LEAF)) {
+                cur = visit(cur);
+                if (cur != kB2Done && (cur & OM_LEAF) && !leaf) { leaf = cur; cur = pop(); }
+                if (__ballot(!leaf && cur != kB2Done) == 0) break;
+            }
+            while (leaf) {
+                test_leaf(recs, leaf_payload(S, leaf, leaves), o, d, tmin, closest, best, w);
+                leaf = 0;
+                if (cur != kB2Done && (cur & OM_LEAF)) { leaf = cur; cur = pop(); }
+            }
+        }
+    } else {
+        while (cur != kB2Done) {
+            if (cur & OM_LEAF) {                        // the single leaf site
+                test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
+                cur = pop();
+            } else {
+                cur = visit(cur);
+            }
+        }
     }
-#undef OM_B2_POP
-#undef OM_B2_PUSH
-    (void)overflow;  // unreachable: om_upload_world enables BVH2 only when depth <= DEPTH
     return best;
 }
 
-
-// Two rays per lane through the LDS BVH2 (OM_WF_DUAL): each iteration issues
-// one 64-B fetch per live ray -- its next node from LDS, or its next leaf record from global
-// memory -- for BOTH rays before either is consumed, then advances each ray by that one step.
-// A lane thus keeps two independent dependent chains in flight (one ray's node or record read
-// overlaps the other's slab or quadratic).  Per ray the visit order, the tests and the
-// acceptance rule are those of traced_bvh2 (near child first, brute-force tie rule), so the
-// winner is bit-identical.  Leaves are walked one record per iteration.
-struct B2Ray {
-    F3 o, d;
-    float ix, iy, iz;
-    float closest;
-    int best;
-    uint32_t cur;          // node to visit when no leaf record is pending
-    uint32_t leaf;         // (next leaf record << 8) | records left; 0: visit node cur
-    int sp;                // lane-stack depth; < 0: the ray is done
-    __device__ __forceinline__ bool live() const { return sp >= 0; }
-};
-
-// Continue at child code c: a node, or a leaf (its records; an empty leaf pops on).
-template <int STRIDE>
-__device__ __forceinline__ void b2_enter(B2Ray& r, uint32_t c, const uint32_t* leaves, const uint16_t* stk) {
-    for (;;) {
-        if (!(c & OM_LEAF)) { r.cur = c; return; }
-        const uint32_t lf = leaves[c & (OM_LEAF - 1u)];        // (OM_WF_DUAL requires OM_B2_DIRECT=0)
-        if (lf & 255u) { r.leaf = lf; return; }
-        if (--r.sp < 0) return;
-        c = stk[r.sp * STRIDE];
-    }
-}
-template <int STRIDE>
-__device__ __forceinline__ void b2_pop(B2Ray& r, const uint32_t* leaves, const uint16_t* stk) {
-    if (--r.sp < 0) return;
-    b2_enter<STRIDE>(r, stk[r.sp * STRIDE], leaves, stk);
-}
-
-// Ray setup: the non-finite answer, or always2 and the root.
-template <class Wk>
-__device__ __forceinline__ void b2_begin(const OmSceneDev& S, B2Ray& r, F3 o, F3 d, float tmin, float tmax, Wk& w) {
-    r.o = o; r.d = d; r.closest = tmax; r.best = -1; r.cur = 0; r.leaf = 0; r.sp = 0;
-    r.ix = r.iy = r.iz = 0.0f;
-    if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) { r.best = nonfinite_hit(S, r.closest); r.sp = -1; return; }
-    r.ix = inv_dir(d.x); r.iy = inv_dir(d.y); r.iz = inv_dir(d.z);
-    offer_always2(S, o, d, tmin, r.ix, r.iy, r.iz, -o.x * r.ix, -o.y * r.iy, -o.z * r.iz, tmin * 0.5f - 1e-3f, r.closest,
-                  r.best, w);
-}
-
-// The 64 B a live ray needs next: a leaf record (global) or a node (LDS).
-__device__ __forceinline__ void b2_fetch(const B2Ray& r, const OmBvh2Node* nodes, const OmAffineTest* recs, uint4 (&q)[4]) {
-    if (!r.live()) return;
-    const uint4* src = r.leaf ? (const uint4*)(recs + (r.leaf >> 8)) : (const uint4*)(nodes + r.cur);
-    q[0] = src[0]; q[1] = src[1]; q[2] = src[2]; q[3] = src[3];
-}
-
-// One step of a live ray with its fetched 64 B.
-template <int DEPTH, int STRIDE, class Wk>
-__device__ __forceinline__ void b2_step(B2Ray& r, const uint4 (&q)[4], const uint32_t* leaves, uint16_t* stk, float tmin,
-                                        Wk& w) {
-    if (!r.live()) return;
-    if (r.leaf) {                                                   // one leaf record
-        OmAffineTest R;
-        __builtin_memcpy(&R, q, sizeof(R));
-        test_rec(R, r.o, r.d, tmin, r.closest, r.best, w);
-        r.leaf += 255u;                                             // next record, one fewer left
-        if (!(r.leaf & 255u)) { r.leaf = 0; b2_pop<STRIDE>(r, leaves, stk); }
-        return;
-    }
-    OmBvh2Node N;                                                   // one node: both child boxes
-    __builtin_memcpy(&N, q, sizeof(N));
-    w.add_pre(2);
-    const float nox = -r.o.x * r.ix, noy = -r.o.y * r.iy, noz = -r.o.z * r.iz;
-    const float t_lo = tmin * 0.5f - 1e-3f, t_hi = r.closest * 1.0001f + 1e-3f;
-    float x0 = __builtin_fmaf(N.lo0[0], r.ix, nox), x1 = __builtin_fmaf(N.hi0[0], r.ix, nox);
-    float y0 = __builtin_fmaf(N.lo0[1], r.iy, noy), y1 = __builtin_fmaf(N.hi0[1], r.iy, noy);
-    float z0 = __builtin_fmaf(N.lo0[2], r.iz, noz), z1 = __builtin_fmaf(N.hi0[2], r.iz, noz);
-    const float n0 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
-    const float f0 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
-    x0 = __builtin_fmaf(N.lo1[0], r.ix, nox); x1 = __builtin_fmaf(N.hi1[0], r.ix, nox);
-    y0 = __builtin_fmaf(N.lo1[1], r.iy, noy); y1 = __builtin_fmaf(N.hi1[1], r.iy, noy);
-    z0 = __builtin_fmaf(N.lo1[2], r.iz, noz); z1 = __builtin_fmaf(N.hi1[2], r.iz, noz);
-    const float n1 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
-    const float f1 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
-    const bool h0 = !(n0 > f0), h1 = !(n1 > f1);
-    if (h0 && h1) {
-        const bool swap = n1 < n0;
-        const uint32_t nearc = swap ? N.c1 : N.c0, farc = swap ? N.c0 : N.c1;
-        if (r.sp < DEPTH) { stk[r.sp * STRIDE] = (uint16_t)farc; ++r.sp; }
-        b2_enter<STRIDE>(r, nearc, leaves, stk);
-    } else if (h0 || h1) {
-        b2_enter<STRIDE>(r, h0 ? N.c0 : N.c1, leaves, stk);
-    } else {
-        b2_pop<STRIDE>(r, leaves, stk);
-    }
-}
-
-// Both rays to completion: -> closest / best of each, as traced_bvh2 would return them.
-template <int DEPTH, int STRIDE, class Wk>
-__device__ __forceinline__ void traced_bvh2_x2(const OmSceneDev& S, const OmBvh2Node* nodes, const uint32_t* leaves,
-                                               const OmAffineTest* recs, uint16_t* stkA, uint16_t* stkB, float tmin,
-                                               B2Ray& A, B2Ray& B, Wk& w) {
-    while (A.live() || B.live()) {
-        uint4 qa[4], qb[4];
-        b2_fetch(A, nodes, recs, qa);
-        b2_fetch(B, nodes, recs, qb);
-        b2_step<DEPTH, STRIDE>(A, qa, leaves, stkA, tmin, w);
-        b2_step<DEPTH, STRIDE>(B, qb, leaves, stkB, tmin, w);
-    }
-}
 
 // 4-wide BVH traversal: one 112-B node read gives four slab tests; the
 // hit children are ordered near-first by a 5-compare sorting network, the nearest is

@@ -1,0 +1,71 @@
+// om_tuning.h — the wavefront pipeline's tunable sizes.  These
+// are numbers, not code variants: every value renders the same bits (results are keyed by slot
+// and (pixel, sample)), and tools/ablate.sh sweeps them by -D.  The measurements behind each
+// default are in DESIGN.md; the code variants that measured slower are gone (git history and
+// DESIGN.md §8 keep their numbers).
+#pragma once
+
+// Workgroup = one queue segment.  512 lanes share one LDS copy of the BVH2 nodes between 8
+// waves, so LDS stops capping occupancy, and 8 waves/SIMD (<= 64 VGPRs) hide the incoherent
+// bounces' latency.  C1 (r01): 256/no hint 3770, 256/8 3671, 512/- 3802, 512/8 3929, 1024/8 3368.
+#ifndef OM_WF_BLOCK
+#define OM_WF_BLOCK 512
+#endif
+#ifndef OM_WF_WAVES
+#define OM_WF_WAVES 8
+#endif
+// queue segments per tail workgroup
+#ifndef OM_WF_TAIL_SPB
+#define OM_WF_TAIL_SPB 2
+#endif
+// paths per batch: 2^OM_WF_MIN_PATHS_LOG2 (16 spp of 1080p), raised to OM_WF_BATCH_SPP samples of
+// the frame for frames above 2M pixels, within 2^OM_WF_MAX_PATHS_LOG2
+#ifndef OM_WF_MAX_PATHS_LOG2
+#define OM_WF_MAX_PATHS_LOG2 27
+#endif
+#ifndef OM_WF_BATCH_SPP
+#define OM_WF_BATCH_SPP 16
+#endif
+#ifndef OM_WF_MIN_PATHS_LOG2
+#define OM_WF_MIN_PATHS_LOG2 25
+#endif
+// A BVH2 too big for LDS (S-10k: 213 KB) stages its breadth-first prefix, up to this many bytes
+// of nodes, into LDS; deeper nodes are read through L2 (0 = every node from L2).
+#ifndef OM_WF_HYB_BYTES
+#define OM_WF_HYB_BYTES 24576
+#endif
+// k_march refills its idle lanes once at least this many of a wave's 64 wait
+#ifndef OM_WF_REFILL
+#define OM_WF_REFILL 16
+#endif
+// k_march: march steps per refill check (the check costs three ballots and its branches).
+// C2 (r03_v16/v17): 1 / 2 / 4 / 6 / 8 steps -> 2500 / 2587 / 2650 / 2661 / 2682 Msamples/s.
+#ifndef OM_MARCH_UNROLL
+#define OM_MARCH_UNROLL 8
+#endif
+// Adaptive calls: samples per pixel per (serial) batch.  C1 adaptive, 16 spp per call:
+// 1 / 4 / 8 / 16 -> 564 / 1519 / 2376 / 3190 credited Msamples/s (megakernel: 2749).
+#ifndef OM_WF_ADAPTIVE_BATCH
+#define OM_WF_ADAPTIVE_BATCH 16
+#endif
+// Queue segments (= bounce workgroups) per CU: OM_WF_LANES_PER_CU / OM_WF_BLOCK; marched worlds
+// and BVH2s read through L2 use the WIDE count.
+#ifndef OM_WF_LANES_PER_CU
+#define OM_WF_LANES_PER_CU 4096
+#endif
+#ifndef OM_WF_LANES_PER_CU_WIDE
+#define OM_WF_LANES_PER_CU_WIDE 8192
+#endif
+// k_accumulate: samples whose loads are issued together before their adds in sample order
+#ifndef OM_ACC_GROUP
+#define OM_ACC_GROUP 8
+#endif
+// k_tail lane refill: bit 0 marched worlds, bit 1 traced worlds; 0 = the r03
+// nested loop (every lane runs its path to completion before it takes another)
+#ifndef OM_WF_TAIL_REFILL
+#define OM_WF_TAIL_REFILL 3
+#endif
+// BVH2 traversal order (om_trace.h traced_bvh2): 1 speculative while-while, 0 if-if
+#ifndef OM_B2_SPECULATIVE
+#define OM_B2_SPECULATIVE 1
+#endif

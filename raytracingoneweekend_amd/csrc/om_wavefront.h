@@ -34,14 +34,6 @@ struct Buffers {
     uint32_t* n0 = nullptr;      // per listed pixel: Stats.n at the start of the call
     uint64_t n0_cap = 0;
     hipStream_t side[kMaxSets] = {};  // streams 1.. of the overlapped schedule
-    hipStream_t tail[2] = {};         // async tails: batch i's tail + accumulate run on tail[i % 2]
-    // accumulate stream (OM_WF_ACC_STREAM): every batch's k_accumulate runs on `acc`, so no
-    // stream waits for the other's accumulate; a second result buffer per set (alt_res, alt_id)
-    // lets batch i + S write its results while batch i's are still being added
-    hipStream_t acc = {};
-    float4* alt_res[kMaxSets] = {};
-    uint32_t* alt_id[kMaxSets] = {};
-    uint64_t alt_cap = 0;
     std::vector<hipEvent_t> ev;  // cross-stream ordering events (timing disabled)
     void release();
 };

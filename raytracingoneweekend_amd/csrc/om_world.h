@@ -42,6 +42,7 @@ struct FrozenWorld {
     std::vector<OmAlwaysRec> always2_rec;  // the same, with their conservative boxes
     std::vector<float> srec_box;       // per srec: inflated box lo xyz, hi xyz (primary-ray tile lists)
     std::vector<OmBvh2Node> b2nodes;   // compressed BVH2 (same leaves/records as snodes)
+    std::vector<OmBvh2NodeH> b2h;      // the same nodes with half-precision boxes rounded outward (device)
     std::vector<uint32_t> b2leaves;    // its leaf table: (first_record << 8) | count
     uint32_t b2_depth = 0;             // its depth (stack bound)
     uint32_t b2_direct = 0;            // 1: leaf child codes carry OM_LEAF | first_record << 4 | count (no table read)

@@ -8,7 +8,7 @@ export TMPDIR=/tmp
 TAG=${1:-pmc}; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
-ARGS="--steps 4 --warmup 1 --no-cpu-baseline $*"
+ARGS="--steps 4 --warmup 1 --no-cpu-baseline --no-window-parity $*"
 i=0
 for PASS in "SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS" \
             "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_FLOPS_FP32 SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_VMEM" \

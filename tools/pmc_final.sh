@@ -1,8 +1,9 @@
 #!/bin/bash
 # End-of-round PMC passes (GPU box), summarised on the box so gpurun_out/ stays small:
 #   C1 all five passes -> pmc_summary_C1.json + pmc_traffic.json; C2 all five -> *_C2.json;
-#   C4 the FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic_C4.json.  Raw pass files are deleted.
-#   [CONFIGS="C1 C2 C4"] bash tools/pmc_final.sh TAG      -> gpurun_out/TAG/pmc_*.json
+#   C3 all five -> *_C3.json; C4 the FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic_C4.json.
+#   Raw pass files are deleted.
+#   [CONFIGS="C1 C2 C3 C4"] bash tools/pmc_final.sh TAG      -> gpurun_out/TAG/pmc_*.json
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 TAG=${1:-pmc_final}
@@ -17,7 +18,8 @@ run() {   # name, passes, bench args...
   python tools/pmc_traffic.py "$OUT/raw_$name" "$OUT/pmc_traffic_$name.json" || return 1
   rm -rf "$OUT/raw_$name"
 }
-case " ${CONFIGS:-C1 C2 C4} " in *" C1 "*) run C1 "1 2 3 4 5" --no-extras || exit 1 ;; esac
-case " ${CONFIGS:-C1 C2 C4} " in *" C2 "*) run C2 "1 2 3 4 5" --config C2 --no-extras || exit 1 ;; esac
-case " ${CONFIGS:-C1 C2 C4} " in *" C4 "*) run C4 "3 4" --config C4 --no-extras || exit 1 ;; esac
+case " ${CONFIGS:-C1 C2 C3 C4} " in *" C1 "*) run C1 "1 2 3 4 5" --no-extras || exit 1 ;; esac
+case " ${CONFIGS:-C1 C2 C3 C4} " in *" C2 "*) run C2 "1 2 3 4 5" --config C2 --no-extras || exit 1 ;; esac
+case " ${CONFIGS:-C1 C2 C3 C4} " in *" C3 "*) run C3 "1 2 3 4 5" --config C3 --no-extras || exit 1 ;; esac
+case " ${CONFIGS:-C1 C2 C3 C4} " in *" C4 "*) run C4 "3 4" --config C4 --no-extras || exit 1 ;; esac
 echo ok
