@@ -126,10 +126,11 @@ __device__ __forceinline__ bool sphere_root(const OmAffineTest& T, F3 o, F3 d, f
 // sqrtd = 0, i.e. a root of +-0, which tmin > 0 rejects either way; everything else
 // (dot products of squares and sums with a nonzero term) is sign-blind.  Callers use it only
 // when tmin > 0; the winner's HitRecord is still built by the full transform.
+template <bool FASTREJ = false>
 __device__ __forceinline__ bool sphere_root_diag(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root) {
     const F3 lo = f3(T.w2l[0] * o.x + T.w2l[3], T.w2l[5] * o.y + T.w2l[7], T.w2l[10] * o.z + T.w2l[11]);
     const F3 ld = f3(T.w2l[0] * d.x + T.dz[0], T.w2l[5] * d.y + T.dz[1], T.w2l[10] * d.z + T.dz[2]);
-    return sphere_root_local(lo, ld, tmin, tmax, root);
+    return sphere_root_local<FASTREJ>(lo, ld, tmin, tmax, root);
 }
 // Cube::hit (traced.rs:266-298) up to (smallest_t, idx).
 __device__ __forceinline__ bool cube_root(const OmAffineTest& T, F3 o, F3 d, float tmin, float tmax, float& root, int& axis) {

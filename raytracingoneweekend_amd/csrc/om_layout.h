@@ -142,7 +142,7 @@ struct OM_ALIGN16 OmBvh2Node {
 };
 #define OM_B2_LO(n, k, i) ((k) == 0 ? (n).lo0[i] : (n).lo1[i])
 #define OM_B2_HI(n, k, i) ((k) == 0 ? (n).hi0[i] : (n).hi1[i])
-// The device form of the same node (32 B, r04): the child boxes as IEEE half-precision bits,
+// The compressed form of the same node (32 B, r04; trees too big for LDS): the child boxes as IEEE half-precision bits,
 // each plane rounded OUTWARD (lo down, hi up) from the f32 box, so a decoded box contains the
 // f32 one and the culling stays conservative (boxes only decide which exact tests run).  A visit
 // reads two 16-B words instead of four, and the slab test's fma takes the halves directly
@@ -174,7 +174,8 @@ struct OmSceneDev {
     uint32_t n_snodes, n_srecs, n_always2;
     uint32_t lds_bytes;           // dynamic LDS the staged kernel needs (0 = scene too big: global path)
     // compressed BVH2 over the same leaves/records as the stackless BVH
-    const OmBvh2NodeH* b2nodes;   // half-precision device nodes (om_bvh.cpp from FrozenWorld::b2nodes)
+    const OmBvh2Node* b2nodes;    // f32 nodes (trees staged whole in LDS; the megakernel)
+    const OmBvh2NodeH* b2h;       // the same nodes with half-precision boxes (trees read through L2)
     const uint32_t* b2leaves;
     const OmAlwaysRec* always2_rec;  // always2 with boxes (BVH2 traversal)
     uint32_t n_b2nodes, n_b2leaves;

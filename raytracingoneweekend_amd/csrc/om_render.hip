@@ -82,17 +82,17 @@ __global__ __launch_bounds__(BLOCK, (BLOCK >= 512 ? 4 : 1)) void render_kernel(O
     const OmAffineTest* lds_recs = (const OmAffineTest*)(om_lds + S.n_snodes * 2u);
     // BVH2: [lane stack][nodes][leaf table] in LDS (nodes through L2 when they exceed the budget)
     uint16_t* b2_stk = (uint16_t*)om_lds + threadIdx.x;
-    const OmBvh2NodeH* b2_nodes = S.b2nodes;
+    const OmBvh2Node* b2_nodes = S.b2nodes;
     const uint32_t* b2_leaves = S.b2leaves;
     if (MODE == MODE_BVH2 && S.b2_lds_bytes) {
         uint4* dst = om_lds + (BLOCK * S.b2_stack * 2u) / 16u;
-        const uint32_t nn = S.n_b2nodes * (uint32_t)(sizeof(OmBvh2NodeH) / 16u);
+        const uint32_t nn = S.n_b2nodes * (uint32_t)(sizeof(OmBvh2Node) / 16u);
         const uint4* sn = (const uint4*)S.b2nodes;
         for (uint32_t i = threadIdx.x; i < nn; i += BLOCK) dst[i] = sn[i];
         uint32_t* ldst = (uint32_t*)(dst + nn);
         for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += BLOCK) ldst[i] = S.b2leaves[i];
         __syncthreads();
-        b2_nodes = (const OmBvh2NodeH*)dst;
+        b2_nodes = (const OmBvh2Node*)dst;
         b2_leaves = ldst;
     }
     const uint32_t tid = blockIdx.x * BLOCK + threadIdx.x;
@@ -623,7 +623,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     UP(tri, tri); UP(plane, plane); UP(para, para);
     UP(msph, msph); UP(mbox, mbox); UP(mtor, mtor);
     UP(mats, mats); UP(bloom, bloom); UP(bvh, bvh); UP(bvh_prims, bvh_prims); UP(always, always);
-    UP(snodes, snodes); UP(srecs, srecs); UP(always2, always2); UP(always2_rec, always2_rec); UP(b2h, b2nodes); UP(b2leaves, b2leaves);
+    UP(snodes, snodes); UP(srecs, srecs); UP(always2, always2); UP(always2_rec, always2_rec); UP(b2nodes, b2nodes); UP(b2h, b2h); UP(b2leaves, b2leaves);
 #undef UP
     c->srec_box = fw.srec_box;
     c->world_gen++;
@@ -645,7 +645,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     S.n_b2leaves = b2_ok ? (uint32_t)fw.b2leaves.size() : 0u;
     S.b2_direct = b2_ok ? fw.b2_direct : 0u;
     S.b2_stack = b2_ok ? fw.b2_depth : 0u;   // one push per internal level on the current path, deepest included
-    const size_t b2_bytes = fw.b2h.size() * sizeof(OmBvh2NodeH) + fw.b2leaves.size() * 4u;
+    const size_t b2_bytes = fw.b2nodes.size() * sizeof(OmBvh2Node) + fw.b2leaves.size() * 4u;
     S.b2_lds_bytes = (b2_ok && b2_bytes <= 40u * 1024u) ? (uint32_t)((b2_bytes + 15u) & ~(size_t)15u) : 0u;
     // BVH4 (same leaf table): up to 3 pushes per level + 3 spare entries for the
     // unconditional pushes, within the 48-entry bound of om_wavefront.hip

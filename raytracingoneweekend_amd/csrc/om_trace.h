@@ -8,10 +8,16 @@
 
 namespace omd {
 
+// Box plane k of a device BVH2 node (k: child 0 lo xyz, hi xyz; child 1 lo xyz, hi xyz).
+template <int K> __device__ __forceinline__ float b2p(const OmBvh2NodeH& N);
+template <int K> __device__ __forceinline__ float b2p(const OmBvh2Node& N) {
+    return K < 3 ? N.lo0[K % 3] : K < 6 ? N.hi0[K % 3] : K < 9 ? N.lo1[K % 3] : N.hi1[K % 3];
+}
 // BVH2 traversal: "no next node" (child codes are 16-bit)
 constexpr uint32_t kB2Done = 0x10000u;
 // A half-precision box plane (OmBvh2NodeH) as f32, exactly.
 __device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
+template <int K> __device__ __forceinline__ float b2p(const OmBvh2NodeH& N) { return h2f(N.b[K]); }
 
 // Slab-test min/max (kept as fminf/fmaxf: an inline-asm v_min/v_max variant that skips
 // LLVM's canonicalising v_max x,x of loop-carried operands measured 12% slower, because the
@@ -205,7 +211,8 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
             if (A.pad == OM_ALWAYS_DIAG_SPHERE && tmin > 0.0f) {
                 float t;
                 w.add_prim();
-                if (sphere_root_diag(uniform_load(S.sph_test + A.gi), o, d, tmin, closest, t) && (t < closest || (int)A.gi > best)) {
+                if (sphere_root_diag<OM_A2_GROUND_FASTREJ != 0>(uniform_load(S.sph_test + A.gi), o, d, tmin, closest, t) &&
+                    (t < closest || (int)A.gi > best)) {
                     closest = t; best = (int)A.gi;
                 }
             } else {
@@ -642,11 +649,11 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
 
 // HYB: only nodes [0, nl) are in `nodes` (the breadth-first prefix staged in LDS); the
 // others are read from `gnodes` (global memory, through L2).
-template <int DEPTH, int STRIDE, class Wk, bool HYB = false>
-__device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2NodeH* nodes, const uint32_t* leaves,
+template <int DEPTH, int STRIDE, class Wk, bool HYB = false, class Node = OmBvh2Node>
+__device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* nodes, const uint32_t* leaves,
                                            const OmAffineTest* recs, uint16_t* stk,
                                            F3 o, F3 d, float tmin, float& closest, Wk& w,
-                                           const OmBvh2NodeH* gnodes = nullptr, uint32_t nl = 0) {
+                                           const Node* gnodes = nullptr, uint32_t nl = 0) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
     const float ix = inv_dir(d.x);
@@ -655,49 +662,47 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
     const float nox = -o.x * ix, noy = -o.y * iy, noz = -o.z * iz;
     const float t_lo = tmin * 0.5f - 1e-3f;
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
-    // one node visit: -> the next code (near child, the only hit child, or a pop; kB2Done when
-    // the stack is empty), the far child pushed.  The stack needs one entry per internal level
-    // on the current path (om_upload_world enables the BVH2 only when its depth <= DEPTH).
-    int sp = 0;
-    auto pop = [&]() -> uint32_t {
-        if (sp == 0) return kB2Done;
-        --sp;
-        return stk[sp * STRIDE];
-    };
-    auto visit = [&](uint32_t node) -> uint32_t {
-        const OmBvh2NodeH N = (HYB && node >= nl) ? gnodes[node] : nodes[node];
+    // slab tests of node N's two child boxes: -> h0, h1 (hit), and whether child 1 is nearer
+    auto slabs = [&](const Node& N, bool& h0, bool& h1, bool& swap) {
         w.add_pre(2);
         const float t_hi = closest * 1.0001f + 1e-3f;
-        // (float)half operands: the fma becomes v_fma_mix_f32 (the conversion is free)
-        float x0 = __builtin_fmaf(h2f(N.b[0]), ix, nox), x1 = __builtin_fmaf(h2f(N.b[3]), ix, nox);
-        float y0 = __builtin_fmaf(h2f(N.b[1]), iy, noy), y1 = __builtin_fmaf(h2f(N.b[4]), iy, noy);
-        float z0 = __builtin_fmaf(h2f(N.b[2]), iz, noz), z1 = __builtin_fmaf(h2f(N.b[5]), iz, noz);
+        // half planes (OmBvh2NodeH): the (float) conversion folds into v_fma_mix_f32
+        float x0 = __builtin_fmaf(b2p<0>(N), ix, nox), x1 = __builtin_fmaf(b2p<3>(N), ix, nox);
+        float y0 = __builtin_fmaf(b2p<1>(N), iy, noy), y1 = __builtin_fmaf(b2p<4>(N), iy, noy);
+        float z0 = __builtin_fmaf(b2p<2>(N), iz, noz), z1 = __builtin_fmaf(b2p<5>(N), iz, noz);
         const float n0 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
         const float f0 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
-        x0 = __builtin_fmaf(h2f(N.b[6]), ix, nox); x1 = __builtin_fmaf(h2f(N.b[9]), ix, nox);
-        y0 = __builtin_fmaf(h2f(N.b[7]), iy, noy); y1 = __builtin_fmaf(h2f(N.b[10]), iy, noy);
-        z0 = __builtin_fmaf(h2f(N.b[8]), iz, noz); z1 = __builtin_fmaf(h2f(N.b[11]), iz, noz);
+        x0 = __builtin_fmaf(b2p<6>(N), ix, nox); x1 = __builtin_fmaf(b2p<9>(N), ix, nox);
+        y0 = __builtin_fmaf(b2p<7>(N), iy, noy); y1 = __builtin_fmaf(b2p<10>(N), iy, noy);
+        z0 = __builtin_fmaf(b2p<8>(N), iz, noz); z1 = __builtin_fmaf(b2p<11>(N), iz, noz);
         const float n1 = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
         const float f1 = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
-        const bool h0 = !(n0 > f0), h1 = !(n1 > f1);
-        if (h0 && h1) {                                 // near child next, far child pushed
-            const bool swap = n1 < n0;
-            if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1); ++sp; }
-            return swap ? N.c1 : N.c0;
-        }
-        if (h0 || h1) return h0 ? N.c0 : N.c1;
-        return pop();
+        h0 = !(n0 > f0); h1 = !(n1 > f1); swap = n1 < n0;
     };
     uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
+    int sp = 0;                                         // lane stack: one entry per internal level
     if constexpr (OM_B2_SPECULATIVE) {
         // speculative while-while (Aila & Laine 2009): the node loop runs until every lane of the
         // wave holds a leaf; a lane that reaches its first leaf postpones it and keeps descending
         // (a second leaf stops it).  Then the lanes test their leaves together.  The winner does
         // not depend on the order of the tests (the tie rule above), so the result is the same.
+        auto pop = [&]() -> uint32_t {
+            if (sp == 0) return kB2Done;
+            --sp;
+            return stk[sp * STRIDE];
+        };
         uint32_t leaf = 0;                              // postponed leaf code (OM_LEAF set), 0 = none
         while (cur != kB2Done || leaf) {
             while (cur != kB2Done && !(cur & OM_LEAF)) {
-                cur = visit(cur);
+                const Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
+                bool h0, h1, swap;
+                slabs(N, h0, h1, swap);
+                if (h0 && h1) {
+                    if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1); ++sp; }
+                    cur = swap ? N.c1 : N.c0;
+                } else {
+                    cur = (h0 || h1) ? (h0 ? N.c0 : N.c1) : pop();
+                }
                 if (cur != kB2Done && (cur & OM_LEAF) && !leaf) { leaf = cur; cur = pop(); }
                 if (__ballot(!leaf && cur != kB2Done) == 0) break;
             }
@@ -708,12 +713,31 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const OmBvh2Node
             }
         }
     } else {
-        while (cur != kB2Done) {
+        // the leaf and node steps of one loop, each ending in `continue`: the structurizer turns
+        // this shape into a node loop nested in the leaf loop (a lane descends until it reaches a
+        // leaf, then the wave's leaves are tested) -- written as one flat if/else loop instead,
+        // C1 ran 14% slower (r04)
+        for (;;) {
             if (cur & OM_LEAF) {                        // the single leaf site
                 test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
-                cur = pop();
+                if (sp == 0) break;
+                --sp;
+                cur = stk[sp * STRIDE];
+                continue;
+            }
+            const Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
+            bool h0, h1, swap;
+            slabs(N, h0, h1, swap);
+            if (h0 && h1) {                             // near child next, far child pushed
+                if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1); ++sp; }
+                cur = swap ? N.c1 : N.c0;
+            } else if (h0 || h1) {
+                cur = h0 ? N.c0 : N.c1;
             } else {
-                cur = visit(cur);
+                if (sp == 0) break;
+                --sp;
+                cur = stk[sp * STRIDE];
+                continue;
             }
         }
     }

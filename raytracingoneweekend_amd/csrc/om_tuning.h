@@ -65,7 +65,11 @@
 #ifndef OM_WF_TAIL_REFILL
 #define OM_WF_TAIL_REFILL 3
 #endif
-// BVH2 traversal order (om_trace.h traced_bvh2): 1 speculative while-while, 0 if-if
+// BVH2 traversal order (om_trace.h traced_bvh2): 1 speculative while-while, 0 the leaf/node loop
 #ifndef OM_B2_SPECULATIVE
-#define OM_B2_SPECULATIVE 1
+#define OM_B2_SPECULATIVE 0
+#endif
+// always2's axis-aligned sphere (the ground) with sphere_root's division-free rejection
+#ifndef OM_A2_GROUND_FASTREJ
+#define OM_A2_GROUND_FASTREJ 0
 #endif

@@ -69,7 +69,6 @@ template <int TR>
 __host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
     return kBlk * ((TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) ? S.b4_stack : S.b2_stack) * 2u;
 }
-constexpr uint32_t kB2Words = sizeof(OmBvh2NodeH) / 16u;                // 16-B words per BVH2 node
 constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
 // marched worlds: 12 (C2, 8 march steps per refill check, r03_v22/v23: T = 6 / 8 / 10 / 12 / 16 / 20
@@ -180,12 +179,14 @@ __device__ __forceinline__ void store_path(const Queue& Q, uint64_t i, const Pat
     st4(Q.qr + i, make_uint4(p.g.s, p.g.k, p.slot, 0u));
 }
 
-// Scene data a workgroup traces against: BVH2/BVH4 nodes + leaf table staged in LDS behind
-// the per-lane stack ([stack][nodes][leaf table]), or read through L2.
+// Scene data a workgroup traces against: the BVH2/BVH4 nodes + leaf table staged in LDS behind
+// the per-lane stack ([stack][nodes][leaf table]), or (TR_BVH2_GLOBAL) the breadth-first prefix
+// of the half-precision nodes in LDS and the rest read through L2.
 struct Tracer {
-    const OmBvh2NodeH* b2n;
-    uint32_t nl;             // TR_BVH2_GLOBAL: nodes [0, nl) staged in LDS at b2l
-    const OmBvh2NodeH* b2l;
+    const OmBvh2Node* b2n;   // TR_BVH2_LDS: f32 nodes in LDS
+    const OmBvh2NodeH* h2l;  // TR_BVH2_GLOBAL: half nodes [0, nl) staged in LDS
+    const OmBvh2NodeH* h2g;  //                 every half node, through L2
+    uint32_t nl;
     const OmBvh4Node* b4n;
     const uint32_t* bl;
     const OmAffineTest* recs;
@@ -197,24 +198,25 @@ __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every 
     Tracer t;
     t.stk = (uint16_t*)wf_lds + threadIdx.x;
     t.b2n = S.b2nodes; t.b4n = S.b4nodes; t.bl = S.b2leaves; t.recs = S.srecs;
-    t.nl = 0; t.b2l = S.b2nodes;
+    t.h2l = S.b2h; t.h2g = S.b2h; t.nl = 0;
     if (TR == TR_BVH2_GLOBAL && hyb_nodes(S)) {
         t.nl = hyb_nodes(S);
         uint4* dst = wf_lds + STACKS * stack_bytes<TR>(S) / 16u;
-        const uint4* sn = (const uint4*)S.b2nodes;
-        for (uint32_t i = threadIdx.x; i < t.nl * kB2Words; i += kBlk) dst[i] = sn[i];
+        const uint4* sn = (const uint4*)S.b2h;
+        for (uint32_t i = threadIdx.x; i < t.nl * (uint32_t)(sizeof(OmBvh2NodeH) / 16u); i += kBlk) dst[i] = sn[i];
         __syncthreads();
-        t.b2l = (const OmBvh2NodeH*)dst;
+        t.h2l = (const OmBvh2NodeH*)dst;
     }
     if (TR == TR_BVH2_LDS || TR == TR_BVH4_LDS) {
-        const uint32_t nn = TR == TR_BVH2_LDS ? S.n_b2nodes * kB2Words : S.n_b4nodes * 7u;   // uint4 per node
+        const uint32_t nn = TR == TR_BVH2_LDS ? S.n_b2nodes * (uint32_t)(sizeof(OmBvh2Node) / 16u)
+                                              : S.n_b4nodes * (uint32_t)(sizeof(OmBvh4Node) / 16u);   // uint4 per node
         const uint4* sn = TR == TR_BVH2_LDS ? (const uint4*)S.b2nodes : (const uint4*)S.b4nodes;
         uint4* dst = wf_lds + STACKS * stack_bytes<TR>(S) / 16u;
         for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = sn[i];
         uint32_t* ldst = (uint32_t*)(dst + nn);
         for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += kBlk) ldst[i] = S.b2leaves[i];
         __syncthreads();
-        t.b2n = (const OmBvh2NodeH*)dst; t.b4n = (const OmBvh4Node*)dst; t.bl = ldst;
+        t.b2n = (const OmBvh2Node*)dst; t.b4n = (const OmBvh4Node*)dst; t.bl = ldst;
     }
     return t;
 }
@@ -230,7 +232,7 @@ __device__ __forceinline__ int trace(const OmSceneDev& S, const OmParamsDev& P, 
     if (TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) best = traced_bvh4<kBlk>(S, T.b4n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
     else if (TR == TR_BVH2_LDS) best = traced_bvh2<kStackDepth, kBlk>(S, T.b2n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
     else if (TR == TR_BVH2_GLOBAL)
-        best = traced_bvh2<kStackDepth, kBlk, Wk, true>(S, T.b2l, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w, T.b2n, T.nl);
+        best = traced_bvh2<kStackDepth, kBlk, Wk, true>(S, T.h2l, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w, T.h2g, T.nl);
     else if (TR == TR_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
     else if (TR == TR_BVH) best = traced_bvh(S, o, d, P.tmin, closest, w);
     else best = traced_brute<TR == TR_CULLED>(S, o, d, P.tmin, closest, w);

@@ -52,9 +52,10 @@ declare -A V=(
   [tr0]="$COMMON $DEV -DOM_WF_TAIL_REFILL=0"
   [tr1]="$COMMON $DEV -DOM_WF_TAIL_REFILL=1"
   [tr2]="$COMMON $DEV -DOM_WF_TAIL_REFILL=2"
-  # BVH2 traversal: if-if (0) instead of the speculative while-while; with the r03 tail
-  [spec0]="$COMMON $DEV -DOM_B2_SPECULATIVE=0"
-  [spec0tr0]="$COMMON $DEV -DOM_B2_SPECULATIVE=0 -DOM_WF_TAIL_REFILL=0"
+  # BVH2 traversal: the speculative while-while instead of the leaf/node loop
+  [spec1]="$COMMON $DEV -DOM_B2_SPECULATIVE=1"
+  # always2's ground sphere with the division-free rejection
+  [gfr1]="$COMMON $DEV -DOM_A2_GROUND_FASTREJ=1"
   # LLVM AMDGPU scheduler strategies (same code, different instruction order)
   [ilp]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-ilp"
   [memclause]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-memory-clause"
