@@ -13,8 +13,6 @@ template <int K> __device__ __forceinline__ float b2p(const OmBvh2NodeH& N);
 template <int K> __device__ __forceinline__ float b2p(const OmBvh2Node& N) {
     return K < 3 ? N.lo0[K % 3] : K < 6 ? N.hi0[K % 3] : K < 9 ? N.lo1[K % 3] : N.hi1[K % 3];
 }
-// BVH2 traversal: "no next node" (child codes are 16-bit)
-constexpr uint32_t kB2Done = 0x10000u;
 // A half-precision box plane (OmBvh2NodeH) as f32, exactly.
 __device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 template <int K> __device__ __forceinline__ float b2p(const OmBvh2NodeH& N) { return h2f(N.b[K]); }
@@ -681,64 +679,31 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
     };
     uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
     int sp = 0;                                         // lane stack: one entry per internal level
-    if constexpr (OM_B2_SPECULATIVE) {
-        // speculative while-while (Aila & Laine 2009): the node loop runs until every lane of the
-        // wave holds a leaf; a lane that reaches its first leaf postpones it and keeps descending
-        // (a second leaf stops it).  Then the lanes test their leaves together.  The winner does
-        // not depend on the order of the tests (the tie rule above), so the result is the same.
-        auto pop = [&]() -> uint32_t {
-            if (sp == 0) return kB2Done;
+    // the leaf and node steps of one loop, each ending in `continue`: the structurizer turns
+    // this shape into a node loop nested in the leaf loop (a lane descends until it reaches a
+    // leaf, then the wave's leaves are tested) -- written as one flat if/else loop instead,
+    // C1 ran 14% slower (r04)
+    for (;;) {
+        if (cur & OM_LEAF) {                        // the single leaf site
+            test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
+            if (sp == 0) break;
             --sp;
-            return stk[sp * STRIDE];
-        };
-        uint32_t leaf = 0;                              // postponed leaf code (OM_LEAF set), 0 = none
-        while (cur != kB2Done || leaf) {
-            while (cur != kB2Done && !(cur & OM_LEAF)) {
-                const Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
-                bool h0, h1, swap;
-                slabs(N, h0, h1, swap);
-                if (h0 && h1) {
-                    if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1); ++sp; }
-                    cur = swap ? N.c1 : N.c0;
-                } else {
-                    cur = (h0 || h1) ? (h0 ? N.c0 : N.c1) : pop();
-                }
-                if (cur != kB2Done && (cur & OM_LEAF) && !leaf) { leaf = cur; cur = pop(); }
-                if (__ballot(!leaf && cur != kB2Done) == 0) break;
-            }
-            while (leaf) {
-                test_leaf(recs, leaf_payload(S, leaf, leaves), o, d, tmin, closest, best, w);
-                leaf = 0;
-                if (cur != kB2Done && (cur & OM_LEAF)) { leaf = cur; cur = pop(); }
-            }
+            cur = stk[sp * STRIDE];
+            continue;
         }
-    } else {
-        // the leaf and node steps of one loop, each ending in `continue`: the structurizer turns
-        // this shape into a node loop nested in the leaf loop (a lane descends until it reaches a
-        // leaf, then the wave's leaves are tested) -- written as one flat if/else loop instead,
-        // C1 ran 14% slower (r04)
-        for (;;) {
-            if (cur & OM_LEAF) {                        // the single leaf site
-                test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
-                if (sp == 0) break;
-                --sp;
-                cur = stk[sp * STRIDE];
-                continue;
-            }
-            const Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
-            bool h0, h1, swap;
-            slabs(N, h0, h1, swap);
-            if (h0 && h1) {                             // near child next, far child pushed
-                if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1); ++sp; }
-                cur = swap ? N.c1 : N.c0;
-            } else if (h0 || h1) {
-                cur = h0 ? N.c0 : N.c1;
-            } else {
-                if (sp == 0) break;
-                --sp;
-                cur = stk[sp * STRIDE];
-                continue;
-            }
+        const Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
+        bool h0, h1, swap;
+        slabs(N, h0, h1, swap);
+        if (h0 && h1) {                             // near child next, far child pushed
+            if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1); ++sp; }
+            cur = swap ? N.c1 : N.c0;
+        } else if (h0 || h1) {
+            cur = h0 ? N.c0 : N.c1;
+        } else {
+            if (sp == 0) break;
+            --sp;
+            cur = stk[sp * STRIDE];
+            continue;
         }
     }
     return best;

@@ -60,15 +60,6 @@
 #ifndef OM_ACC_GROUP
 #define OM_ACC_GROUP 8
 #endif
-// k_tail lane refill: bit 0 marched worlds, bit 1 traced worlds; 0 = the r03
-// nested loop (every lane runs its path to completion before it takes another)
-#ifndef OM_WF_TAIL_REFILL
-#define OM_WF_TAIL_REFILL 3
-#endif
-// BVH2 traversal order (om_trace.h traced_bvh2): 1 speculative while-while, 0 the leaf/node loop
-#ifndef OM_B2_SPECULATIVE
-#define OM_B2_SPECULATIVE 0
-#endif
 // always2's axis-aligned sphere (the ground) with sphere_root's division-free rejection
 #ifndef OM_A2_GROUND_FASTREJ
 #define OM_A2_GROUND_FASTREJ 0

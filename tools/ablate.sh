@@ -48,12 +48,6 @@ declare -A V=(
   [acc1]="$COMMON $DEV -DOM_ACC_GROUP=1"
   [acc4]="$COMMON $DEV -DOM_ACC_GROUP=4"
   [acc16]="$COMMON $DEV -DOM_ACC_GROUP=16"
-  # k_tail lane refill: 0 the r03 nested loop, 1 marched worlds only, 2 traced worlds only
-  [tr0]="$COMMON $DEV -DOM_WF_TAIL_REFILL=0"
-  [tr1]="$COMMON $DEV -DOM_WF_TAIL_REFILL=1"
-  [tr2]="$COMMON $DEV -DOM_WF_TAIL_REFILL=2"
-  # BVH2 traversal: the speculative while-while instead of the leaf/node loop
-  [spec1]="$COMMON $DEV -DOM_B2_SPECULATIVE=1"
   # always2's ground sphere with the division-free rejection
   [gfr1]="$COMMON $DEV -DOM_A2_GROUND_FASTREJ=1"
   # LLVM AMDGPU scheduler strategies (same code, different instruction order)
