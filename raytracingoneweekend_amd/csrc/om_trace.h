@@ -209,8 +209,7 @@ __device__ __forceinline__ void offer_always2(const OmSceneDev& S, F3 o, F3 d, f
             if (A.pad == OM_ALWAYS_DIAG_SPHERE && tmin > 0.0f) {
                 float t;
                 w.add_prim();
-                if (sphere_root_diag<OM_A2_GROUND_FASTREJ != 0>(uniform_load(S.sph_test + A.gi), o, d, tmin, closest, t) &&
-                    (t < closest || (int)A.gi > best)) {
+                if (sphere_root_diag(uniform_load(S.sph_test + A.gi), o, d, tmin, closest, t) && (t < closest || (int)A.gi > best)) {
                     closest = t; best = (int)A.gi;
                 }
             } else {

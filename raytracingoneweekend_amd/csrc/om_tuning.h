@@ -60,7 +60,3 @@
 #ifndef OM_ACC_GROUP
 #define OM_ACC_GROUP 8
 #endif
-// always2's axis-aligned sphere (the ground) with sphere_root's division-free rejection
-#ifndef OM_A2_GROUND_FASTREJ
-#define OM_A2_GROUND_FASTREJ 0
-#endif

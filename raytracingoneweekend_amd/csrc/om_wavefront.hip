@@ -71,9 +71,11 @@ __host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
 }
 constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
-// marched worlds: 12 (C2, 8 march steps per refill check, r03_v22/v23: T = 6 / 8 / 10 / 12 / 16 / 20
-// / 24 -> 2579 / 2647 / 2674 / 2668 / 2655 / 2605 / 2541 Msamples/s, means of two or four runs)
-constexpr uint32_t kTailMarched = 12;
+// marched worlds: 0, i.e. every segment of every path in the lane-refilling tail (k_raygen queues the
+// camera paths, then one k_tail launch; r04): with the refilling tail an earlier start kept winning,
+// C2 T = 12 / 6 / 4 / 3 / 2 / 1 -> 2906 / 3064 / 3081 / 3077 / 3209 / 3274 Msamples/s (r04_sw1-sw3,
+// means of two runs); with the r03 per-path tail the best was 12 (2668)
+constexpr uint32_t kTailMarched = 0;
 // BVH2s read through L2 (S-10k): 10 (C3, r03_v24/v25: T = 6 / 8 / 10 / 12 / 16 / 20 -> 3318 / 3523 /
 // 3553 / 3517 / 3416 / 3351 Msamples/s, means of two to four runs)
 constexpr uint32_t kTailL2 = 10;
@@ -785,7 +787,7 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
             const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
             const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
-            if (bounce > 0 && bounce >= tail_at) return tail(in, cin);
+            if (bounce >= tail_at) return tail(in, cin);             // tail_at 0: the camera paths k_raygen queued
             uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
             const int kc = bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE;
             int ti = each ? tm.begin(st) : -1;

@@ -32,6 +32,10 @@ declare -A V=(
   [hyb0]="$COMMON $DEV -DOM_WF_HYB_BYTES=0"
   [hyb16k]="$COMMON $DEV -DOM_WF_HYB_BYTES=16384"
   [hyb40k]="$COMMON $DEV -DOM_WF_HYB_BYTES=40960"
+  [hyb28k]="$COMMON $DEV -DOM_WF_HYB_BYTES=28672"
+  [hyb8k]="$COMMON $DEV -DOM_WF_HYB_BYTES=8192"
+  [hyb12k]="$COMMON $DEV -DOM_WF_HYB_BYTES=12288"
+  [hyb20k]="$COMMON $DEV -DOM_WF_HYB_BYTES=20480"
   # k_march: refill threshold, steps per refill check
   [refill8]="$COMMON $DEV -DOM_WF_REFILL=8"
   [refill24]="$COMMON $DEV -DOM_WF_REFILL=24"
@@ -48,8 +52,6 @@ declare -A V=(
   [acc1]="$COMMON $DEV -DOM_ACC_GROUP=1"
   [acc4]="$COMMON $DEV -DOM_ACC_GROUP=4"
   [acc16]="$COMMON $DEV -DOM_ACC_GROUP=16"
-  # always2's ground sphere with the division-free rejection
-  [gfr1]="$COMMON $DEV -DOM_A2_GROUND_FASTREJ=1"
   # LLVM AMDGPU scheduler strategies (same code, different instruction order)
   [ilp]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-ilp"
   [memclause]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-memory-clause"
