@@ -322,7 +322,12 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
         flops = (FLOP_EXACT_TEST * ctr.prim_tests + FLOP_BOX_TEST * ctr.pre_tests + FLOP_SEGMENT * ctr.segments
                  + FLOP_CAMERA_RAY * ctr.samples + FLOP_MARCH_STEP * ctr.march_steps)
         if marched and not mega:
-            nbytes = BYTES_PER_SEGMENT_SPLIT * ctr.segments + BYTES_PER_SAMPLE * ctr.samples
+            # split march pipeline with the tail from bounce 1 (the default for marched worlds, r04):
+            # bounce 0 as the split pair (176 B per camera segment), then every later segment in the
+            # lane-refilling tail, whose paths stay in registers: a path entering the tail is written
+            # once and read once (128 B), bounded here by the later segments themselves
+            nbytes = (BYTES_PER_SEGMENT_SPLIT + BYTES_PER_SAMPLE) * ctr.samples \
+                + BYTES_PER_LATER_SEGMENT * (ctr.segments - ctr.samples)
         else:
             nbytes = BYTES_PER_LATER_SEGMENT * (ctr.segments - ctr.samples) + BYTES_PER_SAMPLE * ctr.samples
         achieved_tflops = flops / span_s / 1e12
@@ -336,7 +341,7 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
                 "frac": round(achieved_tflops / PEAK_TFLOPS, 4), "traffic": traffic,
                 "issue_peak": ISSUE_PEAK_TFLOPS, "frac_of_issue_peak": round(achieved_tflops / ISSUE_PEAK_TFLOPS, 4),
                 "kernel": "render_kernel (megakernel)" if mega else
-                          ("k_raygen+k_march+k_bounce<HIT>+k_tail (split march)" if marched else
+                          ("k_raygen+k_march+k_bounce<HIT> (bounce 0) + lane-refilling k_tail" if marched else
                            "k_bounce0+k_bounce+k_tail (fused trace+shade)"),
                 "launches_per_step": round(launches / steps, 2),
                 "avg_launch_ms": round(per_launch_s * 1e3, 4),

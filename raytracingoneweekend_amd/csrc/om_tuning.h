@@ -29,10 +29,11 @@
 #ifndef OM_WF_MIN_PATHS_LOG2
 #define OM_WF_MIN_PATHS_LOG2 25
 #endif
-// A BVH2 too big for LDS (S-10k: 213 KB) stages its breadth-first prefix, up to this many bytes
-// of nodes, into LDS; deeper nodes are read through L2 (0 = every node from L2).
+// A BVH2 too big for LDS (S-10k: 107 KB of half nodes) stages its breadth-first prefix, up to this
+// many bytes of nodes, into LDS; deeper nodes are read through L2 (0 = every node from L2).  C3 with
+// half nodes (r04_ab5/ab6): 8 / 12 / 16 / 20 / 24 / 28 KB -> 4113 / 4137 / 4135 / 4067 / 4069 / 3676.
 #ifndef OM_WF_HYB_BYTES
-#define OM_WF_HYB_BYTES 24576
+#define OM_WF_HYB_BYTES 16384
 #endif
 // k_march refills its idle lanes once at least this many of a wave's 64 wait
 #ifndef OM_WF_REFILL

@@ -71,11 +71,12 @@ __host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
 }
 constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
-// marched worlds: 0, i.e. every segment of every path in the lane-refilling tail (k_raygen queues the
-// camera paths, then one k_tail launch; r04): with the refilling tail an earlier start kept winning,
-// C2 T = 12 / 6 / 4 / 3 / 2 / 1 -> 2906 / 3064 / 3081 / 3077 / 3209 / 3274 Msamples/s (r04_sw1-sw3,
-// means of two runs); with the r03 per-path tail the best was 12 (2668)
-constexpr uint32_t kTailMarched = 0;
+// marched worlds: 1, i.e. bounce 0 as k_march + k_bounce<HIT> (coherent camera rays, lane refill)
+// and every later segment in the lane-refilling tail (r04): C2 T = 12 / 6 / 4 / 3 / 2 / 1 -> 2906 /
+// 3064 / 3081 / 3077 / 3209 / 3274 Msamples/s (r04_sw1-sw3, means of two runs).  The camera rays in
+// the tail as well lost: k_raygen + tail 2772, camera rays generated in the march lanes 2928
+// (r04_ab7); with the r03 per-path tail the best threshold was 12 (2668)
+constexpr uint32_t kTailMarched = 1;
 // BVH2s read through L2 (S-10k): 10 (C3, r03_v24/v25: T = 6 / 8 / 10 / 12 / 16 / 20 -> 3318 / 3523 /
 // 3553 / 3517 / 3416 / 3351 Msamples/s, means of two to four runs)
 constexpr uint32_t kTailL2 = 10;
@@ -539,18 +540,18 @@ struct TailSrc {
     const Queue& in;
     const uint32_t* pre;
     uint32_t s0, segcap;
-    __device__ __forceinline__ void load(uint32_t idx, Path& p) const {
+    __device__ __forceinline__ bool load(uint32_t idx, Path& p) const {
         uint32_t k = 0;
         while (idx >= pre[k + 1]) ++k;
         const uint64_t i = (uint64_t)(s0 + k) * segcap + (idx - pre[k]);
         load_ray(in, i, p);
         load_rest(in, i, p);
+        return true;                                        // (a queued path is always live)
     }
 };
-
-template <int TR, bool COUNT, class M, class Wk>
+template <int TR, bool COUNT, class M, class Src, class Wk>
 __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const OmParamsDev& P, const Tracer& T, const M& m,
-                                                     const TailSrc& src, uint32_t total, uint32_t& next,
+                                                     const Src& src, uint32_t total, uint32_t& next,
                                                      float4* __restrict__ res, uint32_t* __restrict__ res_id, Wk& w) {
     const uint32_t lane = __lane_id();
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
@@ -565,7 +566,7 @@ __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const 
         iters = P.march_steps;
         act = true;
     };
-    if (have) { src.load(idx, p); begin(); }
+    if (have) { have = src.load(idx, p); if (have) begin(); }
     for (;;) {
 #pragma unroll
         for (int u = 0; u < OM_MARCH_UNROLL; ++u) {         // march steps between checks
@@ -590,10 +591,10 @@ __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const 
             base = __builtin_amdgcn_readfirstlane(base);
             if (!have && !dry) {
                 idx = base + (uint32_t)__popcll(want & ((1ull << lane) - 1ull));
-                if (idx < total) { have = true; src.load(idx, p); begin(); } else dry = true;
+                if (idx < total) { have = src.load(idx, p); if (have) begin(); } else dry = true;
             }
         }
-        if (__ballot(have) == 0) break;
+        if (__ballot(have || !dry) == 0) break;             // (a lane not dry is refilled next time round)
     }
     return segs;
 }
@@ -787,7 +788,7 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
             const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
             const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
-            if (bounce >= tail_at) return tail(in, cin);             // tail_at 0: the camera paths k_raygen queued
+            if (bounce > 0 && bounce >= tail_at) return tail(in, cin);
             uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
             const int kc = bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE;
             int ti = each ? tm.begin(st) : -1;
