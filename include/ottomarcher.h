@@ -238,24 +238,25 @@ om_status om_set_counting(om_ctx* ctx, int32_t enable);
  *                          a lane-refilling march launch, then shade), then one persistent
  *                          tail launch, then accumulate
  *   OM_PIPELINE_MEGAKERNEL one persistent-path kernel per call
- *   OM_PIPELINE_AUTO       (default) the faster one measured for the call: megakernel for
- *                          worlds with marched primitives when batches run serially
- *                          (adaptive calls, or om_set_streams 1), else wavefront */
+ *   OM_PIPELINE_AUTO       (default) the faster one measured: the wavefront, for every world,
+ *                          fixed-spp and adaptive calls and any om_set_streams */
 enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1, OM_PIPELINE_AUTO = 2 };
 om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
 /* Wavefront pipeline: bounces >= `bounce` are finished by one persistent tail launch
- * (lanes run whole remaining paths); 0 = default (16; 12 for worlds with marched
+ * (lanes run whole remaining paths); 0 = default (16; 1 for worlds with marched
  * primitives, 10 when the BVH2 is too big for LDS, 24 for batches above 2^25 paths),
  * >= max_depth = no tail.  A pure
  * scheduling knob: results are bit-identical for every value. */
 om_status om_set_tail_bounce(om_ctx* ctx, uint32_t bounce);
 
-/* Wavefront, fixed-spp calls: batches in flight (1..4; default 2).  The call's samples are
- * split into batches of at most 1/streams of the call, dealt round-robin to `streams` HIP
- * streams (the call's stream plus context-owned side streams), each with its own queue set;
- * one batch's latency-bound phases (launch drains, late bounces, tail) then run beside the
- * other's full ones.  Accumulation stays in sample order and the call ends joined on its
- * stream, so results are bit-identical for every value.  1 = one batch after another. */
+/* Wavefront: batches in flight (1..4; default 2).  A fixed-spp call's samples are split into
+ * batches of at most 1/streams of the call (an adaptive call's into batches of 16 samples),
+ * dealt round-robin to `streams` HIP streams (the call's stream plus context-owned side
+ * streams), each with its own queue set; one batch's latency-bound phases (launch drains, late
+ * bounces, tail) then run beside the other's full ones.  An adaptive batch renders the pixels
+ * that retire in the batch beside it speculatively and drops those samples.  Accumulation
+ * stays in sample order and the call ends joined on its stream, so results are bit-identical
+ * for every value.  1 = one batch after another. */
 om_status om_set_streams(om_ctx* ctx, uint32_t streams);
 
 /* Primary rays (wavefront, BVH2): bounce 0 can test, per 8x8 pixel tile, only the leaf

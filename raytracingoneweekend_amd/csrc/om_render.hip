@@ -481,14 +481,10 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     }
     if (threads == 0) return OM_OK;
     int pipeline = c->pipeline;
-    // AUTO: the measured faster pipeline: the megakernel for marched SDFs when
-    // batches run serially (adaptive calls, or om_set_streams(1); C2: 916 vs 790); else the
-    // wavefront (C2 with concurrent batches: 1625 vs 1080, C1: 6100 vs 3142, C1 adaptive with
-    // 16-sample speculative batches: 3190 vs 2749 credited Msamples/s).
-    if (pipeline == OM_PIPELINE_AUTO) {
-        const bool marched = (c->scene.n_msph + c->scene.n_mbox + c->scene.n_mtor) != 0;
-        pipeline = (marched && (p->adaptive || c->wf_streams < 2)) ? OM_PIPELINE_MEGAKERNEL : OM_PIPELINE_WAVEFRONT;
-    }
+    // AUTO: the wavefront, the faster pipeline on every measured config since r04:
+    // C1 6100 vs 3142 Msamples/s, C2 with one stream 2377 vs 1180-1202 (r04_ad), C2 adaptive 2939 vs
+    // 1041 credited (16-sample calls), C1 adaptive 3466 vs 2832 (16-sample calls), 4199 vs 3388 (64).
+    if (pipeline == OM_PIPELINE_AUTO) pipeline = OM_PIPELINE_WAVEFRONT;
     int mode = c->kernel;
     if (mode == OM_KERNEL_AUTO) mode = OM_KERNEL_BVH2;
     if (pipeline == OM_PIPELINE_WAVEFRONT) {

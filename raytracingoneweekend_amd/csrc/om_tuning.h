@@ -39,6 +39,20 @@
 #ifndef OM_WF_REFILL
 #define OM_WF_REFILL 16
 #endif
+// marched tail: a wave shades its ended marches once this many of its lanes wait (1 = at once).
+// C2 (r04_tsh, two runs each): 1 / 4 / 8 / 16 / 32 -> 3244, 3262 / 3284 / 3272, 3293 / 3277, 3278 / 3267
+#ifndef OM_WF_TAIL_SHADE
+#define OM_WF_TAIL_SHADE 8
+#endif
+// marched tail: march steps per check, and the refill threshold (k_march's by default)
+// C2 (r04_tmu, r04_tmu2, two runs each): 4 / 8 / 12 / 16 / 24 / 32 -> 3105 / 3275, 3279 / 3316, 3305 /
+// 3333, 3349, 3361, 3366 / 3399, 3426 / 3399, 3387; refill 8 / 16 / 32 -> 3205, 3200 / 3275, 3279 / 3226, 3247
+#ifndef OM_WF_TAIL_UNROLL
+#define OM_WF_TAIL_UNROLL 24
+#endif
+#ifndef OM_WF_TAIL_REFILL
+#define OM_WF_TAIL_REFILL OM_WF_REFILL
+#endif
 // k_march: march steps per refill check (the check costs three ballots and its branches).
 // C2 (r03_v16/v17): 1 / 2 / 4 / 6 / 8 steps -> 2500 / 2587 / 2650 / 2661 / 2682 Msamples/s.
 #ifndef OM_MARCH_UNROLL

@@ -31,7 +31,7 @@ struct Buffers {
     uint32_t counts_n = 0;       // count words per set
     int nsets = 0;               // sets allocated at `cap`
     QueueSet set[kMaxSets];
-    uint32_t* n0 = nullptr;      // per listed pixel: Stats.n at the start of the call
+    uint32_t* n0 = nullptr;      // per listed pixel (x streams, adaptive): Stats.n snapshots (Gen::n0)
     uint64_t n0_cap = 0;
     hipStream_t side[kMaxSets] = {};  // streams 1.. of the overlapped schedule
     std::vector<hipEvent_t> ev;  // cross-stream ordering events (timing disabled)

@@ -132,8 +132,9 @@ struct Gen {
     const om_pixel_stats* stats;
     const uint32_t* pixels;      // tile-ordered pixel list
     uint32_t n_pixels, by_pixel, batch;
-    const uint32_t* n0;          // fixed-spp calls: Stats.n per listed pixel at the call's start
-    uint32_t done;               // samples of the call before this batch (with n0)
+    const uint32_t* n0;          // concurrent calls: per listed pixel, Stats.n (| retired << 31, adaptive)
+                                 // at a point this batch's stream has already passed
+    uint32_t done;               // samples of the call between that point and this batch (with n0)
     const uint32_t* tile_off;    // primary-ray candidate lists (null: traverse)
     const uint16_t* tile_idx;
     const float* tile_tnear;
@@ -296,14 +297,19 @@ __device__ __forceinline__ bool gen_path(const OmParamsDev& P, const Gen& R, uin
     const uint32_t s_local = (uint32_t)(i / R.n_pixels), k = (uint32_t)(i - (uint64_t)s_local * R.n_pixels);
     pixel = R.pixels[k];
     // the sample index is the pixel's Stats.n (jitters[pixel.stats.n], render_thread.rs:188).
-    // Fixed-spp calls take it from the call-start snapshot plus the samples of earlier
-    // batches, so a batch never waits for the previous batch's accumulate; adaptive
-    // calls (serial batches) read the live Stats for n and the done flag.
+    // Concurrent calls take it from a snapshot plus the samples of the batches after it, so a
+    // batch never waits for the previous batch's accumulate: fixed spp, the call-start snapshot;
+    // adaptive, the state after the last accumulate on this batch's own stream (its retired bit
+    // included).  A pixel that retired in a batch still in flight is rendered speculatively and
+    // its samples are dropped by k_accumulate, in sample order, as in the serial schedule; a
+    // pixel that did not took every sample of those batches, so n + done is its next index.
+    // Serial calls read the live Stats.
     uint32_t s;
     bool live;
     if (R.n0) {
-        s = R.n0[k] + R.done + s_local;
-        live = s < P.spp_total;
+        const uint32_t v = R.n0[k];
+        s = (v & 0x7FFFFFFFu) + R.done + s_local;
+        live = s < P.spp_total && !(v >> 31);
     } else {
         const om_pixel_stats& ps = R.stats[R.by_pixel ? pixel : k];
         s = ps.n + s_local;
@@ -587,7 +593,7 @@ __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const 
     if (have) { have = src.load(idx, p); if (have) begin(); }
     for (;;) {
 #pragma unroll
-        for (int u = 0; u < OM_MARCH_UNROLL; ++u) {         // march steps between checks
+        for (int u = 0; u < OM_WF_TAIL_UNROLL; ++u) {         // march steps between checks
             if (act) {
                 int gi = -1;
                 const int r = marching ? march_step(S, m, p.o, p.d, P.tmax, closest, t, iters, gi, w) : 2;
@@ -597,14 +603,17 @@ __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const 
                 }
             }
         }
-        if (have && !act) {                                 // march ended: handle_hit, next segment or done
+        // march ended: handle_hit, next segment or done -- for the wave's ended lanes together, once
+        // OM_WF_TAIL_SHADE of them wait or none marches
+        const bool ended = have && !act;
+        if (ended && (OM_WF_TAIL_SHADE <= 1 || __popcll(__ballot(ended)) >= OM_WF_TAIL_SHADE || __ballot(act) == 0)) {
             if (COUNT) segs++;
             unpark();
             if (shade_path<true>(S, P, depth_cap, p, closest, best, res, res_id)) begin();
             else have = false;
         }
         const uint64_t want = __ballot(!have && !dry), busy = __ballot(have);
-        if (want && (__popcll(want) >= OM_WF_REFILL || busy == 0)) {
+        if (want && (__popcll(want) >= OM_WF_TAIL_REFILL || busy == 0)) {
             uint32_t base = 0u;
             if (lane == 0) base = atomicAdd(&next, (uint32_t)__popcll(want));
             base = __builtin_amdgcn_readfirstlane(base);
@@ -682,7 +691,7 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
                                                      const uint32_t* __restrict__ pixels, uint32_t n_pixels, uint32_t by_pixel,
                                                      uint32_t batch, const float4* __restrict__ res,
                                                      const uint32_t* __restrict__ res_id, const uint64_t* __restrict__ bloom,
-                                                     unsigned long long* __restrict__ counters) {
+                                                     uint32_t* __restrict__ snap, unsigned long long* __restrict__ counters) {
     const uint32_t k = blockIdx.x * kBlk + threadIdx.x;
     uint32_t n_samples = 0, credited = 0;
     if (k < n_pixels) {
@@ -727,6 +736,7 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
         out.color[0] = (uint8_t)(st.rgbf & 0xFFu); out.color[1] = (uint8_t)((st.rgbf >> 8) & 0xFFu);
         out.color[2] = (uint8_t)((st.rgbf >> 16) & 0xFFu); out.flags = (uint8_t)(st.rgbf >> 24); out.reserved = 0u;
         stats[slot] = out;
+        if (snap) snap[k] = st.n | ((st.rgbf >> 24) & 1u) << 31;   // concurrent adaptive calls (Gen::n0)
     }
     if (COUNT) {
         flush_counter(counters, OMC_SAMPLES, n_samples);
@@ -735,11 +745,16 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
     if (P.progress) flush_counter(counters, OMC_PROGRESS, credited);      // live samples_atom (om_progress)
 }
 
-// k_snapshot: n0[k] = Stats.n of listed pixel k at the start of a fixed-spp call.
+// k_snapshot: n0[c * n_pixels + k] = Stats.n of listed pixel k at the start of a concurrent
+// call (| retired << 31 in adaptive calls), for each of `copies` streams.
 __global__ __launch_bounds__(256) void k_snapshot(const om_pixel_stats* __restrict__ stats, const uint32_t* __restrict__ pixels,
-                                                  uint32_t n_pixels, uint32_t by_pixel, uint32_t* __restrict__ n0) {
+                                                  uint32_t n_pixels, uint32_t by_pixel, uint32_t adaptive, uint32_t copies,
+                                                  uint32_t* __restrict__ n0) {
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
-    if (k < n_pixels) n0[k] = stats[by_pixel ? pixels[k] : k].n;
+    if (k >= n_pixels) return;
+    const om_pixel_stats& ps = stats[by_pixel ? pixels[k] : k];
+    const uint32_t v = ps.n | ((adaptive && (ps.flags & 1u)) ? 0x80000000u : 0u);
+    for (uint32_t c = 0; c < copies; ++c) n0[(uint64_t)c * n_pixels + k] = v;
 }
 
 hipError_t grow(Buffers& B, uint64_t cap, uint32_t counts_n, int nsets) {
@@ -867,16 +882,18 @@ hipError_t ensure_events(Buffers& B, size_t n) {
 }  // namespace
 
 // Schedules:
-//   serial      (adaptive calls, or L.streams == 1) one batch after another on `st`; an
-//               adaptive batch's bounce 0 reads the Stats its predecessor's accumulate wrote.
-//   concurrent  (fixed spp, default) the call's samples split into batches of at most half
+//   serial      (L.streams == 1) one batch after another on `st`; an adaptive batch's bounce 0
+//               reads the Stats its predecessor's accumulate wrote.
+//   concurrent  (default) the call's samples split into batches of at most half
 //               the call, dealt round-robin to L.streams streams (`st` + side streams), each
 //               with its own queue set: two batches are in flight at once, so one batch's
 //               latency-bound phases (the drain of every launch, the late bounces, the tail)
 //               run beside the other's full ones.  Accumulates stay in sample order through
 //               events (acc i after acc i-1) and the call ends joined on `st`.  Sample indices
-//               come from the call-start Stats.n snapshot (n0), so every schedule renders
-//               identical bits.
+//               come from Stats.n snapshots (n0: the call start's, or for adaptive calls the
+//               state after the stream's previous batch), so every schedule renders identical
+//               bits; an adaptive batch renders the pixels that retire in the batch running
+//               beside it speculatively, and k_accumulate drops those samples.
 // Timing: mode 2 brackets the call once on `st` (OM_KT_BOUNCE_SPAN, with the call's
 // bounce-family launch count); mode 1 brackets every launch on its stream and the call.
 hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err) {
@@ -890,10 +907,12 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     const uint64_t kMaxPaths = std::min<uint64_t>(1ull << OM_WF_MAX_PATHS_LOG2,
                                                   std::max<uint64_t>(1ull << OM_WF_MIN_PATHS_LOG2, (uint64_t)OM_WF_BATCH_SPP * n_px));
     const uint32_t want = std::max<uint32_t>(1u, std::min<uint32_t>(L.streams, (uint32_t)kMaxSets));
-    const bool concurrent = !L.P.adaptive && want >= 2u && L.P.sample_count >= 2u;
+    const bool concurrent = want >= 2u && L.P.sample_count >= 2u;
     uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));
     if (L.P.adaptive) batch = std::min<uint32_t>(batch, OM_WF_ADAPTIVE_BATCH);
-    if (concurrent) batch = std::min<uint32_t>(batch, (L.P.sample_count + want - 1u) / want);
+    // fixed spp: at most 1/want of the call per batch, so every call has batches in flight
+    // together; adaptive: full 16-sample batches (a call of 16 samples runs as one)
+    if (concurrent && !L.P.adaptive) batch = std::min<uint32_t>(batch, (L.P.sample_count + want - 1u) / want);
     const uint32_t nb = (L.P.sample_count + batch - 1u) / batch;
     const uint32_t ns = concurrent ? std::min<uint32_t>(want, nb) : 1u;
     const uint32_t depth_cap = L.P.max_depth > 1u ? L.P.max_depth : 1u;
@@ -933,15 +952,20 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     hipStream_t streams[kMaxSets] = {st, st, st, st};
     Timer& tm = *L.timer;
     const int call_ti = tm.begin(st);
-    if (!L.P.adaptive) {
-        if (n_px > B.n0_cap) {
+    // snapshots (Gen::n0): fixed spp, one of the call start; concurrent adaptive, one per stream,
+    // rewritten by every accumulate on that stream.  Serial adaptive calls read the live Stats.
+    const bool adaptive_snaps = L.P.adaptive && concurrent;
+    const uint32_t copies = adaptive_snaps ? ns : 1u;
+    if (!L.P.adaptive || adaptive_snaps) {
+        const uint64_t need = (uint64_t)n_px * copies;
+        if (need > B.n0_cap) {
             if (B.n0) (void)hipFree(B.n0);
             B.n0 = nullptr; B.n0_cap = 0;
-            if ((e = hipMalloc(&B.n0, (size_t)n_px * sizeof(uint32_t))) != hipSuccess) { err = "n0 allocation failed"; return e; }
-            B.n0_cap = n_px;
+            if ((e = hipMalloc(&B.n0, (size_t)need * sizeof(uint32_t))) != hipSuccess) { err = "n0 allocation failed"; return e; }
+            B.n0_cap = need;
         }
         hipLaunchKernelGGL(k_snapshot, dim3((n_px + 255u) / 256u), dim3(256), 0, st, L.stats, L.pixels, n_px,
-                           R.by_pixel, B.n0);
+                           R.by_pixel, L.P.adaptive ? 1u : 0u, copies, B.n0);
         R.n0 = B.n0;
     }
     // events: [0] call start on `st`, [k] side stream k joined, [kMaxSets + i] batch i accumulated
@@ -967,6 +991,14 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
         G.segcap = seg_capacity(paths, nseg);
         R.batch = b;
         R.done = done;
+        uint32_t* snap = nullptr;
+        if (adaptive_snaps) {
+            // batch i reads the snapshot its stream's last accumulate (batch i - ns) wrote, i.e. the
+            // state after batch i - ns; batches i - ns + 1 .. i - 1 (ns - 1 full batches) lie between
+            snap = B.n0 + (uint64_t)(i % ns) * n_px;
+            R.n0 = snap;
+            R.done = i >= ns ? (ns - 1u) * batch : done;
+        }
         switch (tr) {
             case TR_BRUTE: launches += run_tr<TR_BRUTE>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
             case TR_CULLED: launches += run_tr<TR_CULLED>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
@@ -982,10 +1014,10 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
         const int ati = tm.mode == 1 ? tm.begin(si) : -1;
         if (L.count)
             hipLaunchKernelGGL(k_accumulate<true>, dim3(grid_a), dim3(kBlk), 0, si, L.P, L.stats, L.pixels, n_px,
-                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, L.counters);
+                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, snap, L.counters);
         else
             hipLaunchKernelGGL(k_accumulate<false>, dim3(grid_a), dim3(kBlk), 0, si, L.P, L.stats, L.pixels, n_px,
-                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, L.counters);
+                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, snap, L.counters);
         tm.end(ati, OM_KT_ACCUMULATE, si);
         // live progress: the cumulative credit after this batch, to the host word om_progress
         // hands out; ahead of the event the next batch's accumulate waits on, so the copies

@@ -254,19 +254,20 @@ def test_tail_bounce_is_bit_identical(om, oracle, tail):
 
 
 def test_auto_pipeline_choice(om, oracle):
-    """OM_PIPELINE_AUTO: the megakernel for marched SDFs with serial batches (adaptive or one
-    stream), the wavefront otherwise (the faster one measured on C1 / C2 / C1 adaptive,
-    DESIGN.md §5.8), observed through the per-launch timing classes; bit-exact."""
+    """OM_PIPELINE_AUTO: the wavefront for every world, fixed-spp or adaptive, on one stream or
+    two (the faster pipeline on every measured config since r04), observed
+    through the per-launch timing classes; bit-exact."""
     import ctypes as C
     from raytracingoneweekend_amd import _lib as L
     W, H = 24, 16
     for world, oworld, adaptive, streams, want in (
-            (om.marched_scene(), oracle.marched_scene(), False, 1, "megakernel"),
-            (om.marched_scene(), oracle.marched_scene(), False, 2, "bounce0"),
-            (om.marched_scene(), oracle.marched_scene(), True, 2, "megakernel"),
-            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), True, 2, "bounce0"),
-            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, 1, "bounce0"),
-            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, 2, "bounce0")):
+            (om.marched_scene(), oracle.marched_scene(), False, 1, "wavefront"),
+            (om.marched_scene(), oracle.marched_scene(), False, 2, "wavefront"),
+            (om.marched_scene(), oracle.marched_scene(), True, 2, "wavefront"),
+            (om.marched_scene(), oracle.marched_scene(), True, 1, "wavefront"),
+            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), True, 2, "wavefront"),
+            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, 1, "wavefront"),
+            (om.random_scene(0x5EED), oracle.random_scene(0x5EED), False, 2, "wavefront")):
         cam = om.default_camera(W / H)
         fz = world.freeze(cam)                                    # pipeline="auto" is the default
         L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
@@ -277,8 +278,6 @@ def test_auto_pipeline_choice(om, oracle):
         L.check(L.lib.om_get_kernel_times(fz.ctx, C.byref(kt)), fz.ctx)
         mega = kt.launches[L.KT_CLASSES.index("megakernel")]
         wave = sum(kt.launches[L.KT_CLASSES.index(k)] for k in ("bounce0", "bounce", "tail"))
-        # "bounce0": the wavefront pipeline (a marched world's batch may run as one k_march_gen
-        # launch, counted as a tail launch)
         assert (mega > 0 and wave == 0) if want == "megakernel" else (mega == 0 and wave > 0), want
         exp, _ = oracle.render(oworld, oracle.default_camera(W / H),
                                oracle.params(W, H, 8, seed=8, march_steps=256, adaptive=adaptive))
@@ -347,6 +346,31 @@ def test_concurrent_batches_are_bit_identical(om, oracle, streams):
     assert kt.launches[span] > 0 and kt.ms[span] > 0.0
     assert int(pix.pixels["n"].min()) == SPP and int(pix.pixels["n"].max()) == SPP
     assert L.lib.om_set_streams(fz.ctx, 5) == L.OM_ERR_INVALID
+
+
+@pytest.mark.parametrize("streams", [1, 2, 3, 4])
+def test_concurrent_adaptive_batches_are_bit_identical(om, oracle, streams):
+    """Adaptive calls split into batches in flight on 1-4 streams: each batch
+    takes its sample indices and retired bits from the snapshot its stream's previous accumulate
+    wrote, renders the pixels that retire in the batches beside it speculatively, and
+    k_accumulate drops those samples in sample order.  Calls of 7, 16 and 17 samples (one to
+    four batches per call) and a 40-sample call (batches past the first `streams`, which read
+    a snapshot written inside the call) == the sequential oracle."""
+    from raytracingoneweekend_amd import _lib as L
+    W, H, SPP = 72, 40, 40
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    exp, _ = oracle.render(oracle.random_scene(0x5EED), oracle.default_camera(W / H),
+                           oracle.params(W, H, SPP, seed=21, adaptive=True))
+    for counts in ((7, 16, 17), (40,)):
+        fz = world.freeze(cam, kernel="auto", pipeline="wavefront")
+        L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
+        pix = om.PixelsBox.new(W * H)
+        for c in counts:
+            om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=21, adaptive=True, sample_count=c)
+        nb, msg = compare_stats(pix.pixels, exp, f"adaptive streams{streams} calls{counts}")
+        assert nb == 0, msg
+        assert int(pix.pixels["n"].min()) < SPP
 
 
 @pytest.mark.parametrize("pipeline", PIPELINES)

@@ -39,6 +39,21 @@ declare -A V=(
   # k_march: refill threshold, steps per refill check
   [refill8]="$COMMON $DEV -DOM_WF_REFILL=8"
   [refill24]="$COMMON $DEV -DOM_WF_REFILL=24"
+  # marched tail: ended lanes shaded together once this many wait
+  [tsh1]="$COMMON $DEV -DOM_WF_TAIL_SHADE=1"
+  [tsh4]="$COMMON $DEV -DOM_WF_TAIL_SHADE=4"
+  [tsh8]="$COMMON $DEV -DOM_WF_TAIL_SHADE=8"
+  [tsh16]="$COMMON $DEV -DOM_WF_TAIL_SHADE=16"
+  [tsh32]="$COMMON $DEV -DOM_WF_TAIL_SHADE=32"
+  [tmu4]="$COMMON $DEV -DOM_WF_TAIL_UNROLL=4"
+  [tmu12]="$COMMON $DEV -DOM_WF_TAIL_UNROLL=12"
+  [tmu16]="$COMMON $DEV -DOM_WF_TAIL_UNROLL=16"
+  [tmu24]="$COMMON $DEV -DOM_WF_TAIL_UNROLL=24"
+  [tmu32]="$COMMON $DEV -DOM_WF_TAIL_UNROLL=32"
+  [tmu16mu12]="$COMMON $DEV -DOM_WF_TAIL_UNROLL=16 -DOM_MARCH_UNROLL=12"
+  [tmu16mu16]="$COMMON $DEV -DOM_WF_TAIL_UNROLL=16 -DOM_MARCH_UNROLL=16"
+  [trf8]="$COMMON $DEV -DOM_WF_TAIL_REFILL=8"
+  [trf32]="$COMMON $DEV -DOM_WF_TAIL_REFILL=32"
   [mu4]="$COMMON $DEV -DOM_MARCH_UNROLL=4"
   [mu12]="$COMMON $DEV -DOM_MARCH_UNROLL=12"
   # adaptive wavefront: samples per pixel per serial batch

@@ -1,6 +1,7 @@
 """Adaptive sampling (render_thread.rs:31-38, 68-102, 196-198) on C1: a pixel retires after
 5 consecutive samples leave its 8-bit colour unchanged, and the progress counter credits
-the skipped samples.  Per pipeline: wall time for a 64-spp frame in 16-spp calls, samples
+the skipped samples.  Per schedule (wavefront with two concurrent batches, wavefront serial,
+megakernel): wall time for a 64-spp frame in STEP-spp calls (argv[1], default 16), samples
 actually taken, samples credited (the reference's samples_atom) -> one JSON line.
 """
 import ctypes as C
@@ -19,35 +20,44 @@ from raytracingoneweekend_amd import _lib as L  # noqa: E402
 
 
 def main():
-    W, H, SPP, STEP = 1920, 1080, 64, 16
+    W, H, SPP = 1920, 1080, 64
+    STEP = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    scene = sys.argv[2] if len(sys.argv) > 2 else "C1"            # C1 (S-traced) or C2 (S-marched, 256 steps)
+    REPS = 5
     stream = torch.cuda.Stream()
     torch.cuda.set_stream(stream)
     sp = C.c_void_p(stream.cuda_stream)
     cam = om.default_camera(W / H)
-    world = om.random_scene(0x5EED)
-    out = {"frame": f"C1 {W}x{H}, {SPP} spp adaptive, {STEP} spp per call"}
+    world = om.random_scene(0x5EED) if scene == "C1" else om.marched_scene()
+    out = {"frame": f"{scene} {W}x{H}, {SPP} spp adaptive, {STEP} spp per call"}
     frames = {}
-    for pipe in ("wavefront", "megakernel"):
+    for name, pipe, streams in (("wavefront", "wavefront", 2), ("wavefront_serial", "wavefront", 1),
+                                ("megakernel", "megakernel", 1)):
         fz = world.freeze(cam, pipeline=pipe)
+        L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
         st = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
-        p = om.make_params(50, 0.001, 100.0, SPP, W, H, sample_count=STEP, seed=1, adaptive=True)
+        p = om.make_params(50, 0.001, 100.0, SPP, W, H, sample_count=STEP, seed=1, adaptive=True,
+                           march_steps=256)
         L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()), sp), fz.ctx)
         torch.cuda.synchronize()
-        st.zero_()
-        L.check(L.lib.om_reset_counters(fz.ctx, sp), fz.ctx)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(SPP // STEP):
-            L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()), sp), fz.ctx)
-        torch.cuda.synchronize()
-        dt = time.perf_counter() - t0
+        reps = []
+        for _ in range(REPS):                                     # REPS frames, each from zeroed Stats
+            st.zero_()
+            L.check(L.lib.om_reset_counters(fz.ctx, sp), fz.ctx)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(SPP // STEP):
+                L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()), sp), fz.ctx)
+            torch.cuda.synchronize()
+            reps.append(time.perf_counter() - t0)
+        dt = sorted(reps)[len(reps) // 2]                         # median frame
         ctr = L.om_counters()
         L.check(L.lib.om_get_counters(fz.ctx, C.byref(ctr)), fz.ctx)
-        frames[pipe] = st.cpu()
-        out[pipe] = {"s": round(dt, 4), "taken_msamples_s": round(ctr.samples / dt / 1e6, 1),
+        frames[name] = st.cpu()
+        out[name] = {"s": round(dt, 4), "frames_s": [round(x, 4) for x in reps], "taken_msamples_s": round(ctr.samples / dt / 1e6, 1),
                      "credited_msamples_s": round(ctr.credited / dt / 1e6, 1),
                      "taken_frac": round(ctr.samples / (W * H * SPP), 4)}
-    out["pipelines_bit_identical"] = bool(torch.equal(frames["wavefront"], frames["megakernel"]))
+    out["schedules_bit_identical"] = all(bool(torch.equal(frames["wavefront"], f)) for f in frames.values())
     print(json.dumps(out))
 
 
