@@ -53,6 +53,11 @@
 #ifndef OM_WF_TAIL_REFILL
 #define OM_WF_TAIL_REFILL OM_WF_REFILL
 #endif
+// marched worlds: first bounce run by the lane-refilling tail (0: every segment, camera rays
+// included)
+#ifndef OM_WF_TAIL_MARCHED
+#define OM_WF_TAIL_MARCHED 1
+#endif
 // k_march: march steps per refill check (the check costs three ballots and its branches).
 // C2 (r03_v16/v17): 1 / 2 / 4 / 6 / 8 steps -> 2500 / 2587 / 2650 / 2661 / 2682 Msamples/s.
 #ifndef OM_MARCH_UNROLL

@@ -76,7 +76,7 @@ constexpr uint32_t kTailDefault = 16;                             // first bounc
 // 3064 / 3081 / 3077 / 3209 / 3274 Msamples/s (r04_sw1-sw3, means of two runs).  The camera rays in
 // the tail as well lost: k_raygen + tail 2772, camera rays generated in the march lanes 2928
 // (r04_ab7); with the r03 per-path tail the best threshold was 12 (2668)
-constexpr uint32_t kTailMarched = 1;
+constexpr uint32_t kTailMarched = OM_WF_TAIL_MARCHED;
 // BVH2s read through L2 (S-10k): 10 (C3, r03_v24/v25: T = 6 / 8 / 10 / 12 / 16 / 20 -> 3318 / 3523 /
 // 3553 / 3517 / 3416 / 3351 Msamples/s, means of two to four runs)
 constexpr uint32_t kTailL2 = 10;
@@ -822,7 +822,7 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
         for (uint32_t bounce = 0; bounce < depth_cap; ++bounce) {
             const Queue in = queue(B, bounce & 1u), out = queue(B, (bounce + 1u) & 1u);
             const uint32_t* cin = B.counts + (size_t)bounce * G.nseg;
-            if (bounce > 0 && bounce >= tail_at) return tail(in, cin);
+            if (bounce >= tail_at) return tail(in, cin);   // (tail_at 0: k_raygen's camera paths too)
             uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
             const int kc = bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE;
             int ti = each ? tm.begin(st) : -1;
