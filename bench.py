@@ -448,6 +448,7 @@ def main():
         extras["C4"] = config_entry("C4", e, " (N=1 leg of the 8-GPU config: 256 of its 4096 spp)")
         extras["C4"]["cpu_baseline"] = cpu_baseline("C4", min(6.0, args.cpu_budget))
         extras["C0"] = run_c0(args)
+        extras["C1_adaptive"] = run_adaptive(args)
     cpu = None
     if rank == 0 and world_size == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.config, args.cpu_budget)
@@ -487,6 +488,63 @@ def main():
         }
         print(json.dumps(out))
     ctl.close()
+
+
+def run_adaptive(args, spp=512, per_call=128, reps=3):
+    """C1's 1080p frame in the reference's default mode, adaptive sampling (render_thread.rs:31-38,
+    68-102, 196-198): a pixel retires after 5 samples that leave its 8-bit colour unchanged, and
+    the progress counter credits its skipped samples.  value = credited Msamples/s (the
+    reference's samples_atom rate), beside the samples actually taken.  One fresh 512-spp frame in
+    128-spp calls per rep (each call: concurrent 16-sample batches); the frame
+    must be identical across reps and to the serial schedule (bit-exactness vs the oracle:
+    tests/test_gpu_parity.py's adaptive tests)."""
+    W, H = CONFIGS["C1"].get("size", (1920, 1080))
+    stream = torch.cuda.Stream()
+    sp = C.c_void_p(stream.cuda_stream)
+    world = make_scene("S-traced", om)
+    cam = om.default_camera(W / H)
+    frames = {}
+    out = {}
+    for label, streams in (("concurrent", args.streams), ("serial", 1)):
+        fz = world.freeze(cam, kernel=args.kernel, pipeline=args.pipeline)
+        L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
+        st = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
+        p = om.make_params(MAX_DEPTH, TMIN, TMAX, spp, W, H, sample_count=per_call, seed=SEED, adaptive=True)
+
+        def frame():
+            for _ in range(spp // per_call):
+                L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()), sp),
+                        fz.ctx)
+        L.check(L.lib.om_set_counting(fz.ctx, 1), fz.ctx)          # counting pass: samples taken, credit
+        L.check(L.lib.om_reset_counters(fz.ctx, sp), fz.ctx)
+        frame()
+        torch.cuda.synchronize()
+        ctr = L.om_counters()
+        L.check(L.lib.om_get_counters(fz.ctx, C.byref(ctr)), fz.ctx)
+        ref = st.clone()
+        L.check(L.lib.om_set_counting(fz.ctx, 0), fz.ctx)          # production build, timed
+        times = []
+        for _ in range(reps):
+            st.zero_()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            frame()
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+            assert torch.equal(st, ref), "adaptive frame differs between reps / builds"
+        fz.close()
+        dt = sorted(times)[len(times) // 2]
+        frames[label] = ref
+        out[label] = {"credited_msamples_s": round(ctr.credited / dt / 1e6, 3),
+                      "taken_msamples_s": round(ctr.samples / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 4),
+                      "taken_frac": round(ctr.samples / (W * H * spp), 4)}
+    assert torch.equal(frames["concurrent"], frames["serial"]), "adaptive schedules differ"
+    c = out["concurrent"]
+    return {"metric": "credited Msamples/s", "value": c["credited_msamples_s"], "taken_msamples_s": c["taken_msamples_s"],
+            "taken_frac": c["taken_frac"], "ms_per_frame": c["ms_per_frame"],
+            "workload": f"C1 S-traced {W}x{H}, {spp} spp adaptive (the reference's default), {per_call}-spp calls, "
+                        f"depth {MAX_DEPTH}, median of {reps} fresh frames",
+            "serial_batches": out["serial"], "schedules_bit_identical": True}
 
 
 def run_c0(args, reps=20):

@@ -53,8 +53,9 @@
 #ifndef OM_WF_TAIL_REFILL
 #define OM_WF_TAIL_REFILL OM_WF_REFILL
 #endif
-// marched worlds: first bounce run by the lane-refilling tail (0: every segment, camera rays
-// included)
+// marched worlds: first bounce run by the lane-refilling tail (0: the camera paths too; DESIGN.md
+// §5.8).  C2 T = 12 / 6 / 4 / 3 / 2 / 1 -> 2906 / 3064 / 3081 / 3077 / 3209 / 3274 Msamples/s (r04_sw1-
+// sw3, means of two runs); on the tuned tail T = 0 / 1 -> 2843, 2916 / 3425, 3413 (r04_q3)
 #ifndef OM_WF_TAIL_MARCHED
 #define OM_WF_TAIL_MARCHED 1
 #endif

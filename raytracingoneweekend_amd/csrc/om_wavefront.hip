@@ -71,11 +71,8 @@ __host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
 }
 constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
-// marched worlds: 1, i.e. bounce 0 as k_march + k_bounce<HIT> (coherent camera rays, lane refill)
-// and every later segment in the lane-refilling tail (r04): C2 T = 12 / 6 / 4 / 3 / 2 / 1 -> 2906 /
-// 3064 / 3081 / 3077 / 3209 / 3274 Msamples/s (r04_sw1-sw3, means of two runs).  The camera rays in
-// the tail as well lost: k_raygen + tail 2772, camera rays generated in the march lanes 2928
-// (r04_ab7); with the r03 per-path tail the best threshold was 12 (2668)
+// marched worlds: bounce 0 as k_march + k_bounce<HIT>, every later segment in the lane-refilling
+// tail (om_tuning.h)
 constexpr uint32_t kTailMarched = OM_WF_TAIL_MARCHED;
 // BVH2s read through L2 (S-10k): 10 (C3, r03_v24/v25: T = 6 / 8 / 10 / 12 / 16 / 20 -> 3318 / 3523 /
 // 3553 / 3517 / 3416 / 3351 Msamples/s, means of two to four runs)
