@@ -701,7 +701,7 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
         // the loads of OM_ACC_GROUP samples are issued together (ids, then results and bloom
         // words), then added in sample order: one lane's samples no longer cost a chain of
         // dependent global round trips each (r03: 0.2-0.85 ms per 1080p x 16-spp launch before)
-        bool retired = false;
+        bool retired = P.adaptive && (st.rgbf & 0x01000000u);          // retired before the batch: no loads
         for (uint32_t s0 = 0; s0 < batch && !retired; s0 += OM_ACC_GROUP) {
             const uint32_t m = batch - s0 < OM_ACC_GROUP ? batch - s0 : OM_ACC_GROUP;
             uint32_t id[OM_ACC_GROUP];
@@ -908,16 +908,26 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));
     if (L.P.adaptive) batch = std::min<uint32_t>(batch, OM_WF_ADAPTIVE_BATCH);
     // fixed spp: at most 1/want of the call per batch, so every call has batches in flight
-    // together; adaptive: full 16-sample batches (a call of 16 samples runs as one)
+    // together; adaptive: full 16-sample batches (a call of 16 samples runs as one), and the
+    // call's later batches OM_WF_ADAPTIVE_BATCH_LATER samples (within 2^OM_WF_MAX_PATHS_LOG2 paths):
+    // by then most pixels have retired, so a batch's live paths are few
     if (concurrent && !L.P.adaptive) batch = std::min<uint32_t>(batch, (L.P.sample_count + want - 1u) / want);
-    const uint32_t nb = (L.P.sample_count + batch - 1u) / batch;
+    const uint32_t later = L.P.adaptive
+        ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)OM_WF_ADAPTIVE_BATCH_LATER,
+                                                             (1ull << OM_WF_MAX_PATHS_LOG2) / n_px))
+        : batch;
+    std::vector<uint32_t> done_at(1, 0u);                          // samples of the call before batch i
+    while (done_at.back() < L.P.sample_count)
+        done_at.push_back(done_at.back() + std::min(done_at.size() == 1 ? batch : later, L.P.sample_count - done_at.back()));
+    const uint32_t nb = (uint32_t)done_at.size() - 1u;
+    const uint32_t bmax = std::max(batch, nb > 1 ? later : 0u);
     const uint32_t ns = concurrent ? std::min<uint32_t>(want, nb) : 1u;
     const uint32_t depth_cap = L.P.max_depth > 1u ? L.P.max_depth : 1u;
     int dev = 0;
     (void)hipGetDevice(&dev);
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint64_t max_paths = (uint64_t)n_px * batch;
+    const uint64_t max_paths = (uint64_t)n_px * bmax;
     int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
     if (tr == TR_BVH4_LDS) tr = L.S.n_b4nodes == 0 ? TR_BVH2_LDS : (L.S.b4_lds_bytes ? TR_BVH4_LDS : TR_BVH4_GLOBAL);
     // an empty BVH2 (no bounded sphere/cube: marched-only worlds, C2) takes the reference loop
@@ -930,7 +940,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
     const uint32_t tail_at = L.tail_bounce ? L.tail_bounce
                            : march ? kTailMarched : tr == TR_BVH2_GLOBAL ? kTailL2
-                           : max_paths > (1ull << 25) ? kTailBigBatch : kTailDefault;
+                           : (uint64_t)n_px * batch > (1ull << 25) ? kTailBigBatch : kTailDefault;
     const uint32_t lanes_per_cu = (march || tr == TR_BVH2_GLOBAL) ? OM_WF_LANES_PER_CU_WIDE : OM_WF_LANES_PER_CU;
     uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (lanes_per_cu / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
@@ -978,8 +988,8 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
         }
     }
     uint32_t launches = 0;
-    for (uint32_t i = 0, done = 0; i < nb; ++i) {
-        const uint32_t b = std::min(batch, L.P.sample_count - done);
+    for (uint32_t i = 0; i < nb; ++i) {
+        const uint32_t done = done_at[i], b = done_at[i + 1] - done;
         const uint64_t paths = (uint64_t)n_px * b;
         hipStream_t si = streams[i % ns];
         QueueSet& QS = B.set[i % ns];
@@ -991,10 +1001,10 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
         uint32_t* snap = nullptr;
         if (adaptive_snaps) {
             // batch i reads the snapshot its stream's last accumulate (batch i - ns) wrote, i.e. the
-            // state after batch i - ns; batches i - ns + 1 .. i - 1 (ns - 1 full batches) lie between
+            // state after batch i - ns; batches i - ns + 1 .. i - 1 (all full) lie between
             snap = B.n0 + (uint64_t)(i % ns) * n_px;
             R.n0 = snap;
-            R.done = i >= ns ? (ns - 1u) * batch : done;
+            R.done = i >= ns ? done - done_at[i - ns + 1u] : done;
         }
         switch (tr) {
             case TR_BRUTE: launches += run_tr<TR_BRUTE>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
@@ -1024,7 +1034,6 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
                                  hipMemcpyDeviceToHost, si);
         if (ns > 1) (void)hipEventRecord(B.ev[kMaxSets + i], si);
         if ((e = hipGetLastError()) != hipSuccess) { err = "wavefront launch failed"; return e; }
-        done += b;
     }
     for (uint32_t k = 1; k < ns; ++k) {
         (void)hipEventRecord(B.ev[k], streams[k]);

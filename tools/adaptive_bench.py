@@ -20,8 +20,9 @@ from raytracingoneweekend_amd import _lib as L  # noqa: E402
 
 
 def main():
-    W, H, SPP = 1920, 1080, 64
+    W, H = 1920, 1080
     STEP = int(sys.argv[1]) if len(sys.argv) > 1 else 16
+    SPP = int(sys.argv[3]) if len(sys.argv) > 3 else 64
     scene = sys.argv[2] if len(sys.argv) > 2 else "C1"            # C1 (S-traced) or C2 (S-marched, 256 steps)
     REPS = 5
     stream = torch.cuda.Stream()
@@ -38,6 +39,7 @@ def main():
         st = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
         p = om.make_params(50, 0.001, 100.0, SPP, W, H, sample_count=STEP, seed=1, adaptive=True,
                            march_steps=256)
+        L.check(L.lib.om_set_counting(fz.ctx, 0), fz.ctx)          # timed: the production build
         L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()), sp), fz.ctx)
         torch.cuda.synchronize()
         reps = []
@@ -51,6 +53,14 @@ def main():
             torch.cuda.synchronize()
             reps.append(time.perf_counter() - t0)
         dt = sorted(reps)[len(reps) // 2]                         # median frame
+        timed = st.clone()
+        st.zero_()                                                # counting pass: samples taken, credit
+        L.check(L.lib.om_set_counting(fz.ctx, 1), fz.ctx)
+        L.check(L.lib.om_reset_counters(fz.ctx, sp), fz.ctx)
+        for _ in range(SPP // STEP):
+            L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()), sp), fz.ctx)
+        torch.cuda.synchronize()
+        assert torch.equal(st, timed), "counting build changed the frame"
         ctr = L.om_counters()
         L.check(L.lib.om_get_counters(fz.ctx, C.byref(ctr)), fz.ctx)
         frames[name] = st.cpu()
