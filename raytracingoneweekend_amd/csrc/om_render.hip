@@ -483,7 +483,8 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
     int pipeline = c->pipeline;
     // AUTO: the wavefront, the faster pipeline on every measured config since r04:
     // C1 6100 vs 3142 Msamples/s, C2 with one stream 2377 vs 1180-1202 (r04_ad), C2 adaptive 2939 vs
-    // 1041 credited (16-sample calls), C1 adaptive 3466 vs 2832 (16-sample calls), 4199 vs 3388 (64).
+    // 1041 credited (16-sample calls), C1 adaptive 3466 vs 2832 (16-sample calls), 4199 vs 3388 (64),
+    // all counting build; production build, C1 adaptive 64 spp in one call: 7171 vs 3392-3507 (r04_q7).
     if (pipeline == OM_PIPELINE_AUTO) pipeline = OM_PIPELINE_WAVEFRONT;
     int mode = c->kernel;
     if (mode == OM_KERNEL_AUTO) mode = OM_KERNEL_BVH2;

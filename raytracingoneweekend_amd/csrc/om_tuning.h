@@ -69,12 +69,12 @@
 #ifndef OM_WF_ADAPTIVE_BATCH
 #define OM_WF_ADAPTIVE_BATCH 16
 #endif
-// Adaptive calls: samples per pixel of the call's batches after the first (by then most pixels
-// have retired and a batch's live paths are few).  C1 adaptive, credited Msamples/s (r04_q5):
-// 512 spp in 128-spp calls 16 / 32 / 64 -> 9827, 9844 / 10828, 11088 / 11597, 11782; 64 spp in one
-// call 16 / 64 -> 4238, 4207 / 5030, 5018 (counting build, tools/adaptive_bench.py)
+// Adaptive calls: samples per pixel of the call's batches after the first.  C1 adaptive, 512 spp in
+// 128-spp calls, credited Msamples/s with the production build timed (r04_q7): 16 / 32 / 64 -> 18590,
+// 18510 / 15891, 15878 / 14613, 14613 (fewer, bigger batches overlap worse); 64 spp in one call
+// 16 / 64 -> 7171, 7189 / 6515, 6567.  (The counting build had ranked them the other way round.)
 #ifndef OM_WF_ADAPTIVE_BATCH_LATER
-#define OM_WF_ADAPTIVE_BATCH_LATER 64
+#define OM_WF_ADAPTIVE_BATCH_LATER 16
 #endif
 // Queue segments (= bounce workgroups) per CU: OM_WF_LANES_PER_CU / OM_WF_BLOCK; marched worlds
 // and BVH2s read through L2 use the WIDE count.

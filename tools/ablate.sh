@@ -61,6 +61,7 @@ declare -A V=(
   # adaptive wavefront: samples per pixel per serial batch
   [ab4]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=4"
   [ab8]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=8"
+  [al16]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH_LATER=16"
   [al32]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH_LATER=32"
   [al64]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH_LATER=64"
   # batch shape: 2^25 paths for every frame (C4 in 4-spp batches), 8 / 32-spp batches
