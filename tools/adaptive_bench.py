@@ -32,8 +32,9 @@ def main():
     world = om.random_scene(0x5EED) if scene == "C1" else om.marched_scene()
     out = {"frame": f"{scene} {W}x{H}, {SPP} spp adaptive, {STEP} spp per call"}
     frames = {}
-    for name, pipe, streams in (("wavefront", "wavefront", 2), ("wavefront_serial", "wavefront", 1),
-                                ("megakernel", "megakernel", 1)):
+    extra = [int(x) for x in sys.argv[4].split(",")] if len(sys.argv) > 4 else []   # more stream counts
+    for name, pipe, streams in ([("wavefront", "wavefront", 2), ("wavefront_serial", "wavefront", 1),
+                                 ("megakernel", "megakernel", 1)] + [(f"wavefront_s{k}", "wavefront", k) for k in extra]):
         fz = world.freeze(cam, pipeline=pipe)
         L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
         st = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
