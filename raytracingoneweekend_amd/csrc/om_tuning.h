@@ -59,14 +59,6 @@
 #ifndef OM_WF_TAIL_MARCHED
 #define OM_WF_TAIL_MARCHED 1
 #endif
-// marched worlds: bounce 0 as one k_march_shade launch (march + shade, survivors compacted) instead
-// of k_march + k_bounce<HIT>, and its march steps per check
-#ifndef OM_WF_MARCH_SHADE
-#define OM_WF_MARCH_SHADE 0
-#endif
-#ifndef OM_WF_MS_UNROLL
-#define OM_WF_MS_UNROLL OM_MARCH_UNROLL
-#endif
 // k_march: march steps per refill check (the check costs three ballots and its branches).
 // C2 (r03_v16/v17): 1 / 2 / 4 / 6 / 8 steps -> 2500 / 2587 / 2650 / 2661 / 2682 Msamples/s.
 #ifndef OM_MARCH_UNROLL

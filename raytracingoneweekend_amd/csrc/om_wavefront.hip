@@ -552,28 +552,10 @@ struct TailSrc {
         return true;                                        // (a queued path is always live)
     }
 };
-// The paths of one queue segment (k_march_shade).
-struct SegSrc {
-    const Queue& in;
-    uint64_t seg0;
-    __device__ __forceinline__ bool load(uint32_t idx, Path& p) const {
-        load_ray(in, seg0 + idx, p);
-        load_rest(in, seg0 + idx, p);
-        return true;
-    }
-};
-// ONE (k_march_shade): a path's survivor after its first shade is appended to segment `oseg0` of
-// `out` (wave-aggregated LDS counter q_out) instead of marching on in its lane.
-struct OneOut {
-    Queue out;
-    uint64_t oseg0;
-    uint32_t* q_out;
-};
-template <int TR, bool COUNT, int UNROLL = OM_WF_TAIL_UNROLL, bool ONE = false, class M, class Src, class Wk>
+template <int TR, bool COUNT, class M, class Src, class Wk>
 __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const OmParamsDev& P, const Tracer& T, const M& m,
                                                      const Src& src, uint32_t total, uint32_t& next,
-                                                     float4* __restrict__ res, uint32_t* __restrict__ res_id, Wk& w,
-                                                     const OneOut* so = nullptr) {
+                                                     float4* __restrict__ res, uint32_t* __restrict__ res_id, Wk& w) {
     const uint32_t lane = __lane_id();
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
     uint32_t idx = threadIdx.x, segs = 0, iters = 0;
@@ -608,7 +590,7 @@ __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const 
     if (have) { have = src.load(idx, p); if (have) begin(); }
     for (;;) {
 #pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {                    // march steps between checks
+        for (int u = 0; u < OM_WF_TAIL_UNROLL; ++u) {         // march steps between checks
             if (act) {
                 int gi = -1;
                 const int r = marching ? march_step(S, m, p.o, p.d, P.tmax, closest, t, iters, gi, w) : 2;
@@ -624,20 +606,8 @@ __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const 
         if (ended && (OM_WF_TAIL_SHADE <= 1 || __popcll(__ballot(ended)) >= OM_WF_TAIL_SHADE || __ballot(act) == 0)) {
             if (COUNT) segs++;
             unpark();
-            const bool keep = shade_path<true>(S, P, depth_cap, p, closest, best, res, res_id);
-            if constexpr (ONE) {
-                const uint64_t km = __ballot(keep);                // among the lanes shading now
-                if (km) {
-                    uint32_t obase = 0u;
-                    if (lane == (uint32_t)__ffsll((long long)__ballot(true)) - 1u) obase = atomicAdd(so->q_out, (uint32_t)__popcll(km));
-                    obase = __builtin_amdgcn_readfirstlane(obase);
-                    if (keep) store_path(so->out, so->oseg0 + obase + (uint32_t)__popcll(km & ((1ull << lane) - 1ull)), p);
-                }
-                have = false;
-            } else {
-                if (keep) begin();
-                else have = false;
-            }
+            if (shade_path<true>(S, P, depth_cap, p, closest, best, res, res_id)) begin();
+            else have = false;
         }
         const uint64_t want = __ballot(!have && !dry), busy = __ballot(have);
         if (want && (__popcll(want) >= OM_WF_TAIL_REFILL || busy == 0)) {
@@ -704,44 +674,6 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmPar
             if (__ballot(have) == 0) break;
         }
     }
-    if (COUNT) {
-        flush_counter(counters, OMC_SEGMENTS, segs);
-        flush_counter(counters, OMC_PRIM_TESTS, w.prim);
-        flush_counter(counters, OMC_PRE_TESTS, w.pre);
-        flush_counter(counters, OMC_MARCH, w.march);
-    }
-}
-
-// k_march_shade (OM_WF_MARCH_SHADE): bounce 0 of a marched world in one launch, k_march's lane
-// refill with the shade inside it (the tail's loop, one segment per path): survivors are compacted
-// into segment s of `out`, no hit buffer, no k_bounce<HIT>.
-template <int TR, bool COUNT, int VIEW>
-__global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_march_shade(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
-                                                      const uint32_t* __restrict__ count_in, Queue out,
-                                                      uint32_t* __restrict__ count_out, float4* __restrict__ res,
-                                                      uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters) {
-    const uint32_t n = count_in[blockIdx.x];
-    if (n == 0) {
-        if (threadIdx.x == 0) count_out[blockIdx.x] = 0u;
-        return;
-    }
-    __shared__ uint32_t next, q_out;
-    if (threadIdx.x == 0) { next = kBlk; q_out = 0u; }
-    __syncthreads();
-    const Tracer T = stage_scene<TR>(S);
-    const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
-    const SegSrc src{in, seg0};
-    const OneOut so{out, seg0, &q_out};
-    WorkT<COUNT> w;
-    uint32_t segs;
-    if constexpr (VIEW == MV_EXACT_C2_LDS) {
-        __shared__ MarchedC2Lds::Block mblock;
-        segs = tail_march_lanes<TR, COUNT, OM_WF_MS_UNROLL, true>(S, P, T, MarchedC2Lds(S, &mblock), src, n, next, res, res_id, w, &so);
-    } else {
-        segs = tail_march_lanes<TR, COUNT, OM_WF_MS_UNROLL, true>(S, P, T, MarchedArrays(S), src, n, next, res, res_id, w, &so);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) count_out[blockIdx.x] = q_out;
     if (COUNT) {
         flush_counter(counters, OMC_SEGMENTS, segs);
         flush_counter(counters, OMC_PRIM_TESTS, w.prim);
@@ -891,18 +823,6 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
             uint32_t* cout = B.counts + (size_t)(bounce + 1u) * G.nseg;
             const int kc = bounce == 0 ? OM_KT_BOUNCE0 : OM_KT_BOUNCE;
             int ti = each ? tm.begin(st) : -1;
-            if (OM_WF_MARCH_SHADE && bounce == 0) {
-                if (exact && exact_view_built<TR>())
-                    hipLaunchKernelGGL((k_march_shade<TR, COUNT, exact_view_built<TR>() ? MV_EXACT_C2_LDS : MV_ARRAYS>),
-                                       dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G, in, cin, out, cout, B.res, B.res_id,
-                                       L.counters);
-                else
-                    hipLaunchKernelGGL((k_march_shade<TR, COUNT, MV_ARRAYS>), dim3(G.nseg), dim3(kBlk), lds, st, L.S, L.P, G,
-                                       in, cin, out, cout, B.res, B.res_id, L.counters);
-                tm.end(ti, kc, st);
-                ++launches;
-                continue;
-            }
             if (exact && exact_view_built<TR>())
                 hipLaunchKernelGGL((k_march<TR, COUNT, exact_view_built<TR>() ? MV_EXACT_C2_LDS : MV_ARRAYS>), dim3(G.nseg),
                                    dim3(kBlk), lds, st, L.S, L.P, G, in, cin, B.hit, L.counters);

@@ -40,9 +40,6 @@ declare -A V=(
   [refill8]="$COMMON $DEV -DOM_WF_REFILL=8"
   [refill24]="$COMMON $DEV -DOM_WF_REFILL=24"
   # marched tail: ended lanes shaded together once this many wait
-  [ms1]="$COMMON $DEV -DOM_WF_MARCH_SHADE=1"
-  [ms1u16]="$COMMON $DEV -DOM_WF_MARCH_SHADE=1 -DOM_WF_MS_UNROLL=16"
-  [ms1u24]="$COMMON $DEV -DOM_WF_MARCH_SHADE=1 -DOM_WF_MS_UNROLL=24"
   [tm0]="$COMMON $DEV -DOM_WF_TAIL_MARCHED=0"
   [tm0l16]="$COMMON $DEV -DOM_WF_TAIL_MARCHED=0 -DOM_WF_LANES_PER_CU_WIDE=16384"
   [tsh1]="$COMMON $DEV -DOM_WF_TAIL_SHADE=1"
