@@ -234,3 +234,38 @@ def test_multi_render_host_sees_a_rewritten_buffer(om, oracle):
     nb, msg = compare_stats(buf, exp, "render_host")
     assert nb == 0, msg
     mf.close()
+
+
+def test_multi_adaptive_shards_bit_identical(om, oracle):
+    """Adaptive calls on shards: each logical rank renders its listed pixels
+    with concurrent 16-sample batches from per-stream snapshots of ITS shard; the gathered frame ==
+    one ctx rendering the whole frame adaptively, and a window of it == the sequential oracle."""
+    import torch
+    from raytracingoneweekend_amd import _lib as L
+    from raytracingoneweekend_amd import shard
+    W, H, SPP, seed = 160, 96, 40, 17
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    p = om.make_params(50, 0.001, 100.0, SPP, W, H, sample_count=SPP, seed=seed, adaptive=True)
+    fz = world.freeze(cam)
+    ref = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
+    L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(ref.data_ptr()), None), fz.ctx)
+    torch.cuda.synchronize()
+    fz.close()
+    mf = shard.MultiFrame([0, 0, 0], world)
+    s = torch.cuda.Stream()
+    frame = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    mf.render(cam, p, frame.data_ptr(), s.cuda_stream)
+    mf.gather(frame.data_ptr(), W, H, s.cuda_stream)
+    s.synchronize()
+    mf.close()
+    assert torch.equal(frame, ref), f"{int((frame != ref).view(-1, 40).any(1).sum())} pixels differ"
+    host = frame.cpu().numpy()
+    assert int(host.view(om.PIXEL_STATS_DTYPE)["n"].min()) < SPP          # pixels retired early
+    pix = np.array([(40 + j) * W + 60 + i for j in range(16) for i in range(16)], dtype=np.uint32)
+    exp = oracle.render_pixels(oracle.random_scene(0x5EED), oracle.default_camera(W / H),
+                               oracle.params(W, H, SPP, seed=seed, adaptive=True), pix)
+    got = host.reshape(W * H, 40)[pix].copy().view(oracle.PIXEL_STATS_DTYPE).reshape(-1)
+    nb, msg = compare_stats(got, exp, "adaptive shards window")
+    assert nb == 0, msg
