@@ -68,6 +68,8 @@ declare -A V=(
   [mp25]="$COMMON $DEV -DOM_WF_MAX_PATHS_LOG2=25"
   [bs8]="$COMMON $DEV -DOM_WF_BATCH_SPP=8 -DOM_WF_MIN_PATHS_LOG2=20"
   [bs32]="$COMMON $DEV -DOM_WF_BATCH_SPP=32"
+  [mn24]="$COMMON $DEV -DOM_WF_MIN_PATHS_LOG2=24"
+  [mn26]="$COMMON $DEV -DOM_WF_MIN_PATHS_LOG2=26"
   # k_accumulate: loads of 1 / 4 / 16 samples issued together
   [acc1]="$COMMON $DEV -DOM_ACC_GROUP=1"
   [acc4]="$COMMON $DEV -DOM_ACC_GROUP=4"
