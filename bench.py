@@ -116,7 +116,10 @@ def cpu_baseline(cfg, budget_s, lib="liboro.so", threads=0, dump=None):
 
 def pmc_fields(name):
     """VALU lane utilisation and wait fractions of the bounce family from the committed per-kernel
-    PMC summary of this config ("also report ... VALU utilization"), or None."""
+    PMC summary of this config ("also report ... VALU utilization"), or None.
+    The summary names the library build it profiled (om_build_id); `matches_timed_build` says
+    whether that is the build timed here (an A/B build must not carry another build's
+    counters as its own, so the caller reports them at the top level only when it matches)."""
     f = PMC_SUMMARY.format(name)
     if not os.path.exists(f):
         return None
@@ -132,12 +135,19 @@ def pmc_fields(name):
     tot = sum(wc.values()) or 1.0
     for k in per:
         per[k]["wave_cycle_share"] = round(wc.get(k, 0.0) / tot, 4)
+    build = pm.get("build_id")
     return {"valu_lane_utilisation": round(comb["valu_lane_utilisation"], 4),
             "wait_any_frac": round(comb["wait_any_frac"], 4), "wait_inst_frac": round(comb["wait_inst_frac"], 4),
-            "per_kernel": per, "source": pm.get("source"), "file": os.path.relpath(f, ROOT)}
+            "per_kernel": per, "source": pm.get("source"), "file": os.path.relpath(f, ROOT),
+            "build_id": build, "matches_timed_build": build is not None and build == L.build_id()}
 
 
-def window_parity(name, frame_u8, W, H, spp, depth, march_steps):
+def pmc_top(pmc, key):
+    """A PMC field for the top level of a roofline: only when the summary profiled this build."""
+    return pmc[key] if pmc and pmc["matches_timed_build"] else None
+
+
+def window_parity(name, frame_u8, W, H, spp, depth, march_steps, adaptive=False):
     """One window of the timed frame (rank 0, after the timed region) vs the oracle's render of it
     (oracle/cpu_bench.py --window in a child process: the oracle never enters this process)."""
     import tempfile
@@ -146,7 +156,8 @@ def window_parity(name, frame_u8, W, H, spp, depth, march_steps):
     with tempfile.TemporaryDirectory() as td:
         dump = os.path.join(td, "window.npy")
         r = subprocess.run([sys.executable, os.path.join(ROOT, "oracle", "cpu_bench.py"), "--config", name,
-                            "--window", f"{W},{H},{x0},{y0},{size},{spp}", "--dump", dump, "--threads", "-1"],
+                            "--window", f"{W},{H},{x0},{y0},{size},{spp},{int(adaptive)}", "--dump", dump,
+                            "--threads", "-1"],
                            capture_output=True, text=True, timeout=600)
         if r.returncode != 0:
             raise RuntimeError(f"oracle window {name} failed: {r.stderr[-2000:]}")
@@ -157,7 +168,7 @@ def window_parity(name, frame_u8, W, H, spp, depth, march_steps):
     bad = int(np.any(got != exp, axis=1).sum())
     if bad:
         print(f"bench: {name} window parity FAILED: {bad}/{pix.size} pixels differ from the oracle", file=sys.stderr)
-    return {"window": [int(x0), int(y0), size], "spp": spp, "depth": depth, "pixels": int(pix.size),
+    return {"window": [int(x0), int(y0), size], "spp": spp, "depth": depth, "pixels": int(pix.size), "adaptive": adaptive,
             "bit_exact_vs_oracle": bad == 0, "pixels_differ": bad, "oracle_s": info["seconds"],
             "objects_hit": int(np.count_nonzero(got.view(np.uint64)[:, 0]))}
 
@@ -351,8 +362,8 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
                 "hbm_achieved_gbs": round(nbytes / span_s / 1e9, 2), "traffic_source": traffic_src,
                 "traffic_over_algorithmic": round(traffic / (nbytes / launches), 3) if traffic else None,
                 "kernel_share_of_step": round(span_s / elapsed, 4), "timing": timing_mode,
-                "valu_lane_utilisation": pmc["valu_lane_utilisation"] if pmc else None,
-                "wait_any_frac": pmc["wait_any_frac"] if pmc else None, "pmc": pmc,
+                "valu_lane_utilisation": pmc_top(pmc, "valu_lane_utilisation"),
+                "wait_any_frac": pmc_top(pmc, "wait_any_frac"), "pmc": pmc,
                 "all_kernels_ms_per_step": {k: round(kl.ms[i] / steps, 4) for i, k in enumerate(L.KT_CLASSES)
                                             if kl.launches[i]}}
     return {
@@ -495,9 +506,10 @@ def run_adaptive(args, spp=512, per_call=128, reps=3):
     68-102, 196-198): a pixel retires after 5 samples that leave its 8-bit colour unchanged, and
     the progress counter credits its skipped samples.  value = credited Msamples/s (the
     reference's samples_atom rate), beside the samples actually taken.  One fresh 512-spp frame in
-    128-spp calls per rep (each call: concurrent 16-sample batches); the frame
-    must be identical across reps and to the serial schedule (bit-exactness vs the oracle:
-    tests/test_gpu_parity.py's adaptive tests)."""
+    128-spp calls per rep (each call: the live pixels dealt to the streams, each stream's batches
+    planned on the device from its live list); the frame must be identical across
+    reps and to the serial schedule, and its centre window to the oracle's adaptive render
+    (window_parity); the roofline is the counting pass's executed work over the median frame."""
     W, H = CONFIGS["C1"].get("size", (1920, 1080))
     stream = torch.cuda.Stream()
     sp = C.c_void_p(stream.cuda_stream)
@@ -505,6 +517,7 @@ def run_adaptive(args, spp=512, per_call=128, reps=3):
     cam = om.default_camera(W / H)
     frames = {}
     out = {}
+    ctrs = {}
     for label, streams in (("concurrent", args.streams), ("serial", 1)):
         fz = world.freeze(cam, kernel=args.kernel, pipeline=args.pipeline)
         L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
@@ -515,12 +528,13 @@ def run_adaptive(args, spp=512, per_call=128, reps=3):
             for _ in range(spp // per_call):
                 L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()), sp),
                         fz.ctx)
-        L.check(L.lib.om_set_counting(fz.ctx, 1), fz.ctx)          # counting pass: samples taken, credit
+        L.check(L.lib.om_set_counting(fz.ctx, 1), fz.ctx)          # counting pass: samples taken, credit, work
         L.check(L.lib.om_reset_counters(fz.ctx, sp), fz.ctx)
         frame()
         torch.cuda.synchronize()
         ctr = L.om_counters()
         L.check(L.lib.om_get_counters(fz.ctx, C.byref(ctr)), fz.ctx)
+        ctrs[label] = ctr
         ref = st.clone()
         L.check(L.lib.om_set_counting(fz.ctx, 0), fz.ctx)          # production build, timed
         times = []
@@ -537,13 +551,39 @@ def run_adaptive(args, spp=512, per_call=128, reps=3):
         frames[label] = ref
         out[label] = {"credited_msamples_s": round(ctr.credited / dt / 1e6, 3),
                       "taken_msamples_s": round(ctr.samples / dt / 1e6, 3), "ms_per_frame": round(dt * 1e3, 4),
-                      "taken_frac": round(ctr.samples / (W * H * spp), 4)}
+                      "taken_frac": round(ctr.samples / (W * H * spp), 4),
+                      "gsegments_per_s": round(ctr.segments / dt / 1e9, 3)}
     assert torch.equal(frames["concurrent"], frames["serial"]), "adaptive schedules differ"
     c = out["concurrent"]
+    ctr = ctrs["concurrent"]
+    dt = c["ms_per_frame"] / 1e3
+    parity = None
+    if not args.no_window_parity:
+        parity = window_parity("C1", frames["concurrent"].cpu().numpy(), W, H, spp, MAX_DEPTH, 1024, adaptive=True)
+    # executed work of the frame (counting pass; speculative samples included in the segments and
+    # tests, camera rays priced at the samples taken: a lower bound) over the median frame time
+    flops = (FLOP_EXACT_TEST * ctr.prim_tests + FLOP_BOX_TEST * ctr.pre_tests + FLOP_SEGMENT * ctr.segments
+             + FLOP_CAMERA_RAY * ctr.samples)
+    nbytes = BYTES_PER_LATER_SEGMENT * max(0, ctr.segments - ctr.samples) + BYTES_PER_SAMPLE * ctr.samples
+    pmc = pmc_fields("C1_adaptive")
+    achieved = flops / dt / 1e12
+    roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / PEAK_TFLOPS, 4), "frac_of_issue_peak": round(achieved / ISSUE_PEAK_TFLOPS, 4),
+            "kernel": "k_bounce0+k_bounce+k_tail (fused trace+shade), adaptive live-list batches",
+            "timing": "median frame wall time (host clock around the 4 calls)",
+            "flop_per_frame": round(flops), "algorithmic_bytes_per_frame": round(nbytes),
+            "hbm_achieved_gbs": round(nbytes / dt / 1e9, 2),
+            "valu_lane_utilisation": pmc_top(pmc, "valu_lane_utilisation"),
+            "wait_any_frac": pmc_top(pmc, "wait_any_frac"), "pmc": pmc}
     return {"metric": "credited Msamples/s", "value": c["credited_msamples_s"], "taken_msamples_s": c["taken_msamples_s"],
             "taken_frac": c["taken_frac"], "ms_per_frame": c["ms_per_frame"],
             "workload": f"C1 S-traced {W}x{H}, {spp} spp adaptive (the reference's default), {per_call}-spp calls, "
                         f"depth {MAX_DEPTH}, median of {reps} fresh frames",
+            "work": {"segments_per_taken_sample": round(ctr.segments / max(1, ctr.samples), 4),
+                     "prim_tests_per_segment": round(ctr.prim_tests / max(1, ctr.segments), 3),
+                     "box_tests_per_segment": round(ctr.pre_tests / max(1, ctr.segments), 3),
+                     "gsegments_per_s": c["gsegments_per_s"]},
+            "roofline": roof, "window_parity": parity,
             "serial_batches": out["serial"], "schedules_bit_identical": True}
 
 

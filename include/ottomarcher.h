@@ -244,20 +244,30 @@ enum { OM_PIPELINE_MEGAKERNEL = 0, OM_PIPELINE_WAVEFRONT = 1, OM_PIPELINE_AUTO =
 om_status om_set_pipeline(om_ctx* ctx, int32_t pipeline);
 /* Wavefront pipeline: bounces >= `bounce` are finished by one persistent tail launch
  * (lanes run whole remaining paths); 0 = default (16; 1 for worlds with marched
- * primitives, 10 when the BVH2 is too big for LDS, 24 for batches above 2^25 paths),
+ * primitives, 10 when the BVH2 is too big for LDS, 8 for adaptive calls, 24 for batches
+ * above 2^25 paths),
  * >= max_depth = no tail.  A pure
  * scheduling knob: results are bit-identical for every value. */
 om_status om_set_tail_bounce(om_ctx* ctx, uint32_t bounce);
 
 /* Wavefront: batches in flight (1..4; default 2).  A fixed-spp call's samples are split into
- * batches of at most 1/streams of the call (an adaptive call's into batches of 16 samples),
- * dealt round-robin to `streams` HIP streams (the call's stream plus context-owned side
- * streams), each with its own queue set; one batch's latency-bound phases (launch drains, late
- * bounces, tail) then run beside the other's full ones.  An adaptive batch renders the pixels
- * that retire in the batch beside it speculatively and drops those samples.  Accumulation
- * stays in sample order and the call ends joined on its stream, so results are bit-identical
- * for every value.  1 = one batch after another. */
+ * batches of at most 1/streams of the call, dealt round-robin to `streams` HIP streams (the
+ * call's stream plus context-owned side streams), each with its own queue set; one batch's
+ * latency-bound phases (launch drains, late bounces, tail) then run beside the other's full
+ * ones.  An adaptive call deals the listed pixels to the streams instead (64-entry chunks), and
+ * each stream renders its live pixels in batches planned on the device (om_set_adaptive_batches).
+ * Accumulation stays in sample order and the call ends joined on its stream, so results are
+ * bit-identical for every value.  1 = one batch after another. */
 om_status om_set_streams(om_ctx* ctx, uint32_t streams);
+
+/* Wavefront adaptive calls (the GPU form of ThreadPixels, render_thread.rs:68-102): each stream
+ * keeps a list of its live pixels, compacted by every batch's accumulate, and runs at most
+ * `batches` batches per call (0 = default 3; more when a batch would exceed 2^26 paths).  A
+ * batch renders b samples of every listed pixel: enough for 2^paths_log2 paths (0 = default 23),
+ * at least an even share of the call's remaining samples over the batches left, at most the
+ * remainder; samples past a pixel's retirement inside a batch are dropped in sample order.  A
+ * pure scheduling knob: results are bit-identical for every value. */
+om_status om_set_adaptive_batches(om_ctx* ctx, uint32_t batches, uint32_t paths_log2);
 
 /* Primary rays (wavefront, BVH2): bounce 0 can test, per 8x8 pixel tile, only the leaf
  * records a conservative lens-aware frustum of the tile reaches, instead of traversing

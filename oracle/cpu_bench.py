@@ -104,13 +104,17 @@ def run(cfg, budget_s, threads, spp_total=64, seed=1, dump=None):
 
 
 def window(cfg, spec, threads, dump, seed=1):
-    """The oracle's Stats of one window of the config's frame (bench.py's window parity)."""
-    w, h, x0, y0, size, spp = (int(v) for v in spec.split(","))
-    p = O.params(w, h, spp, max_depth=DEPTH.get(cfg, 50), seed=seed, march_steps=MARCH.get(cfg, 1024))
+    """The oracle's Stats of one window of the config's frame (bench.py's window parity); a 7th
+    field 1 renders it adaptively (render_thread.rs:31-38, 68-102)."""
+    v = [int(x) for x in spec.split(",")]
+    w, h, x0, y0, size, spp = v[:6]
+    adaptive = len(v) > 6 and v[6] == 1
+    p = O.params(w, h, spp, max_depth=DEPTH.get(cfg, 50), seed=seed, march_steps=MARCH.get(cfg, 1024), adaptive=adaptive)
     t0 = time.perf_counter()
     st = O.render_pixels(scene(cfg), O.default_camera(w / h), p, O.window_pixels(w, h, x0, y0, size), nthreads=threads)
     np.save(dump, st, allow_pickle=False)
-    return {"seconds": round(time.perf_counter() - t0, 3), "threads": threads, "window": [x0, y0, size], "spp": spp}
+    return {"seconds": round(time.perf_counter() - t0, 3), "threads": threads, "window": [x0, y0, size], "spp": spp,
+            "adaptive": adaptive}
 
 
 if __name__ == "__main__":
@@ -120,7 +124,7 @@ if __name__ == "__main__":
     ap.add_argument("--threads", type=int, default=0,
                     help="0: num_cpus::get() - 1 as main.rs:170; -1: num_cpus::get() (the all-cores point)")
     ap.add_argument("--dump", default=None, help="save the rendered Stats (.npy) here")
-    ap.add_argument("--window", default=None, help="W,H,X0,Y0,SIZE,SPP: render one window into --dump")
+    ap.add_argument("--window", default=None, help="W,H,X0,Y0,SIZE,SPP[,ADAPTIVE]: render one window into --dump")
     a = ap.parse_args()
     n = num_cpus()[0]
     t = a.threads if a.threads > 0 else (n if a.threads < 0 else max(1, n - 1))

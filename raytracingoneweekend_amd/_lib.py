@@ -72,7 +72,7 @@ EXPORTS = [
     "om_world_random_scene", "om_world_basic_scene", "om_world_marched_scene", "om_create", "om_destroy",
     "om_last_error", "om_upload_world", "om_set_kernel", "om_render", "om_render_device",
     "om_render_device_pixels", "om_get_counters", "om_reset_counters", "om_set_counting", "om_set_pipeline",
-    "om_set_tail_bounce", "om_set_streams", "om_set_timing", "om_get_kernel_times", "om_display_device", "om_display",
+    "om_set_tail_bounce", "om_set_streams", "om_set_adaptive_batches", "om_set_timing", "om_get_kernel_times", "om_display_device", "om_display",
     "om_write_bmp", "om_write_ppm", "om_set_primary_lists",
     "om_shard_capacity", "om_shard_pixels", "om_shard_assemble_host", "om_comm_unique_id", "om_comm_init_rank",
     "om_comm_destroy", "om_comm_info", "om_render_shard", "om_gather_frame", "om_scatter_frame", "om_multi_create",
@@ -158,6 +158,7 @@ def _load():
         "om_set_pipeline": (st, [vp, C.c_int32]),
         "om_set_tail_bounce": (st, [vp, C.c_uint32]),
         "om_set_streams": (st, [vp, C.c_uint32]),
+        "om_set_adaptive_batches": (st, [vp, C.c_uint32, C.c_uint32]),
         "om_set_timing": (st, [vp, C.c_int32]),
         "om_get_kernel_times": (st, [vp, C.POINTER(om_kernel_times)]),
         "om_display_device": (st, [vp, vp, C.c_uint32, C.c_uint32, C.c_int32, vp, vp]),

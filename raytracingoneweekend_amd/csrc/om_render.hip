@@ -271,7 +271,8 @@ struct om_ctx {
     bool count_work = true;
     int pipeline = OM_PIPELINE_AUTO;
     uint32_t tail_bounce = 0;
-    uint32_t wf_streams = 2;            // wavefront fixed-spp calls: batches in flight (om_set_streams)
+    uint32_t wf_streams = 2;            // wavefront calls: batches in flight (om_set_streams)
+    uint32_t ad_batches = 0, ad_paths_log2 = 0;   // adaptive wavefront schedule (om_set_adaptive_batches; 0 = default)
     // primary-ray tile lists (om_tiles.h): host record boxes of the uploaded world, the
     // device lists of the last (camera, frame, world) and the policy (om_set_primary_lists)
     std::vector<float> srec_box;
@@ -497,6 +498,7 @@ om_status launch(om_ctx* c, const om_camera* cam, const om_render_params* p, om_
         L.count = c->count_work;
         L.tail_bounce = c->tail_bounce;
         L.streams = c->wf_streams;
+        L.ad_batches = c->ad_batches; L.ad_paths_log2 = c->ad_paths_log2;
         L.timer = &c->timer;
         L.tile_off = nullptr; L.tile_idx = nullptr; L.tile_tnear = nullptr;
         L.progress_host = c->progress_host;
@@ -755,6 +757,14 @@ om_status om_set_streams(om_ctx* c, uint32_t streams) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
     if (streams < 1 || streams > (uint32_t)omw::kMaxSets) return set_err(c, OM_ERR_INVALID, "om_set_streams: streams must be 1..4");
     c->wf_streams = streams;
+    return OM_OK;
+}
+
+om_status om_set_adaptive_batches(om_ctx* c, uint32_t batches, uint32_t paths_log2) {
+    if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
+    if (batches > 4096u || paths_log2 > 27u)
+        return set_err(c, OM_ERR_INVALID, "om_set_adaptive_batches: batches <= 4096, paths_log2 <= 27");
+    c->ad_batches = batches; c->ad_paths_log2 = paths_log2;
     return OM_OK;
 }
 

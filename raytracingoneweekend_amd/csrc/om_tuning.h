@@ -40,9 +40,10 @@
 #define OM_WF_REFILL 16
 #endif
 // marched tail: a wave shades its ended marches once this many of its lanes wait (1 = at once).
-// C2 (r04_tsh, two runs each): 1 / 4 / 8 / 16 / 32 -> 3244, 3262 / 3284 / 3272, 3293 / 3277, 3278 / 3267
+// r04's sweep ran with a ballot that made every value behave as 1; with the ballots
+// fixed (r05_p1, C2, two runs each): 1 / 8 / 16 -> 3422, 3389 / 3407, 3384 / 3377, 3360: no gain, 1.
 #ifndef OM_WF_TAIL_SHADE
-#define OM_WF_TAIL_SHADE 8
+#define OM_WF_TAIL_SHADE 1
 #endif
 // marched tail: march steps per check, and the refill threshold (k_march's by default)
 // C2 (r04_tmu, r04_tmu2, two runs each): 4 / 8 / 12 / 16 / 24 / 32 -> 3105 / 3275, 3279 / 3316, 3305 /
@@ -64,17 +65,25 @@
 #ifndef OM_MARCH_UNROLL
 #define OM_MARCH_UNROLL 8
 #endif
-// Adaptive calls: samples per pixel per (serial) batch.  C1 adaptive, 16 spp per call:
-// 1 / 4 / 8 / 16 -> 564 / 1519 / 2376 / 3190 credited Msamples/s (megakernel: 2749).
-#ifndef OM_WF_ADAPTIVE_BATCH
-#define OM_WF_ADAPTIVE_BATCH 16
+// Adaptive calls: the live pixels are dealt to the streams by 64-entry chunks of the
+// call's pixel list, and each stream renders ITS pixels in at most OM_WF_ADAPTIVE_BATCHES batches per
+// call, from a live list its own k_accumulate compacts (ThreadPixels, render_thread.rs:68-102).  A
+// batch's sample count is planned on the device from the stream's live count c: enough samples to
+// give 2^OM_WF_ADAPTIVE_PATHS_LOG2 paths (c x b), at least an even share of the call's remaining
+// samples over the batches left, at most the remainder.
+#ifndef OM_WF_ADAPTIVE_BATCHES
+#define OM_WF_ADAPTIVE_BATCHES 3
 #endif
-// Adaptive calls: samples per pixel of the call's batches after the first.  C1 adaptive, 512 spp in
-// 128-spp calls, credited Msamples/s with the production build timed (r04_q7): 16 / 32 / 64 -> 18590,
-// 18510 / 15891, 15878 / 14613, 14613 (fewer, bigger batches overlap worse); 64 spp in one call
-// 16 / 64 -> 7171, 7189 / 6515, 6567.  (The counting build had ranked them the other way round.)
-#ifndef OM_WF_ADAPTIVE_BATCH_LATER
-#define OM_WF_ADAPTIVE_BATCH_LATER 16
+#ifndef OM_WF_ADAPTIVE_PATHS_LOG2
+#define OM_WF_ADAPTIVE_PATHS_LOG2 23
+#endif
+// the queue capacity an adaptive call may raise its forced even share to (more batches beyond it)
+#ifndef OM_WF_ADAPTIVE_CAP_LOG2
+#define OM_WF_ADAPTIVE_CAP_LOG2 26
+#endif
+// tail threshold for adaptive batches (the per-bounce launches of a light batch are latency-bound)
+#ifndef OM_WF_ADAPTIVE_TAIL
+#define OM_WF_ADAPTIVE_TAIL 8
 #endif
 // Queue segments (= bounce workgroups) per CU: OM_WF_LANES_PER_CU / OM_WF_BLOCK; marched worlds
 // and BVH2s read through L2 use the WIDE count.

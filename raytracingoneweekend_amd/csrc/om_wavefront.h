@@ -31,7 +31,7 @@ struct Buffers {
     uint32_t counts_n = 0;       // count words per set
     int nsets = 0;               // sets allocated at `cap`
     QueueSet set[kMaxSets];
-    uint32_t* n0 = nullptr;      // per listed pixel (x streams, adaptive): Stats.n snapshots (Gen::n0)
+    uint32_t* n0 = nullptr;      // fixed spp: per listed pixel, the call-start Stats.n (Gen::n0); adaptive: live lists + plans
     uint64_t n0_cap = 0;
     hipStream_t side[kMaxSets] = {};  // streams 1.. of the overlapped schedule
     std::vector<hipEvent_t> ev;  // cross-stream ordering events (timing disabled)
@@ -84,7 +84,9 @@ struct Launch {
     bool count;
     int trace_mode;              // closest-hit kernel variant (om_render.hip MODE_*)
     uint32_t tail_bounce;        // first bounce run by the persistent tail kernel (0 = default)
-    uint32_t streams;            // fixed-spp calls: batches in flight (queue sets, streams), 1 = serial, <= kMaxSets
+    uint32_t streams;            // batches in flight (queue sets, streams), 1 = serial, <= kMaxSets
+    uint32_t ad_batches;         // adaptive calls: batches per stream per call (0 = OM_WF_ADAPTIVE_BATCHES)
+    uint32_t ad_paths_log2;      // adaptive calls: log2 of the target paths per batch (0 = OM_WF_ADAPTIVE_PATHS_LOG2)
     Timer* timer;                // per-launch event timing (may be off)
     const uint32_t* tile_off;    // primary-ray candidate lists per 8x8 tile (null = traverse the BVH)
     const uint16_t* tile_idx;

@@ -50,6 +50,7 @@ void Buffers::release() {
     if (n0) (void)hipFree(n0);
     n0 = nullptr; n0_cap = 0;
     for (auto& st : side) { if (st) (void)hipStreamDestroy(st); st = nullptr; }
+
     for (auto e : ev) (void)hipEventDestroy(e);
     ev.clear();
     cap = 0; counts_n = 0; nsets = 0;
@@ -117,6 +118,33 @@ struct Seg {
     uint32_t segcap;  // paths per segment
 };
 
+// Adaptive calls: per stream and batch, the stream's live pixels listed for the
+// batch (c, counted by the previous k_accumulate's compaction) and the call's samples rendered
+// before it (done).  The batch's sample count is a function of the two, evaluated by every kernel
+// of the batch (ad_batch), so the host never reads the count back.
+struct AdPlan { uint32_t c, done; };
+struct AdCfg {
+    uint32_t sample_count;   // samples of the call
+    uint32_t batches;        // batches per stream per call
+    uint32_t paths;          // target paths per batch (c x b)
+};
+__host__ __device__ inline uint32_t ad_batch(uint32_t c, uint32_t done, uint32_t j, const AdCfg& A) {
+    if (c == 0u || done >= A.sample_count || j >= A.batches) return 0u;
+    const uint32_t rem = A.sample_count - done, left = A.batches - j;
+    const uint32_t even = (rem + left - 1u) / left, want = A.paths / c;
+    const uint32_t b = even > want ? even : want;
+    return b < rem ? b : rem;
+}
+// a batch's adaptive list: the live list, its plan, the stream's next list and plan
+struct AdList {
+    const uint32_t* list;    // null: fixed-spp batch over the whole pixel list
+    const AdPlan* plan;
+    uint32_t* list_next;
+    AdPlan* plan_next;
+    AdCfg A;
+    uint32_t j;              // batch index within the stream's call
+};
+
 // One SoA path queue: o|depthf, d|first_id, throughput|segment, rng s|rng k|slot|-.
 struct Queue {
     float4* q0; float4* q1; float4* q2; uint4* qr;
@@ -129,9 +157,9 @@ struct Gen {
     const om_pixel_stats* stats;
     const uint32_t* pixels;      // tile-ordered pixel list
     uint32_t n_pixels, by_pixel, batch;
-    const uint32_t* n0;          // concurrent calls: per listed pixel, Stats.n (| retired << 31, adaptive)
-                                 // at a point this batch's stream has already passed
-    uint32_t done;               // samples of the call between that point and this batch (with n0)
+    const uint32_t* n0;          // concurrent fixed-spp calls: per listed pixel, Stats.n at the call start
+    uint32_t done;               // samples of the call before this batch (with n0)
+    AdList ad;                   // adaptive calls: the stream's live list (ad.list null otherwise)
     const uint32_t* tile_off;    // primary-ray candidate lists (null: traverse)
     const uint16_t* tile_idx;
     const float* tile_tnear;
@@ -289,18 +317,17 @@ __device__ __forceinline__ bool shade_path(const OmSceneDev& S, const OmParamsDe
 
 // Camera sample i of the batch (render_thread.rs:176-192): -> p (a fresh path) and its
 // pixel; false (and no sample recorded in res_id) when the sample is not taken.
-__device__ __forceinline__ bool gen_path(const OmParamsDev& P, const Gen& R, uint64_t i, Path& p, uint32_t& pixel,
-                                         uint32_t* __restrict__ res_id) {
-    const uint32_t s_local = (uint32_t)(i / R.n_pixels), k = (uint32_t)(i - (uint64_t)s_local * R.n_pixels);
+// `stride` is the batch's pixel count: the whole list (fixed spp) or the stream's live list.
+__device__ __forceinline__ bool gen_path(const OmParamsDev& P, const Gen& R, uint32_t stride, uint64_t i, Path& p,
+                                         uint32_t& pixel, uint32_t* __restrict__ res_id) {
+    const uint32_t s_local = (uint32_t)i / stride, kk = (uint32_t)i - s_local * stride;
+    const uint32_t k = R.ad.list ? R.ad.list[kk] : kk;
     pixel = R.pixels[k];
     // the sample index is the pixel's Stats.n (jitters[pixel.stats.n], render_thread.rs:188).
-    // Concurrent calls take it from a snapshot plus the samples of the batches after it, so a
-    // batch never waits for the previous batch's accumulate: fixed spp, the call-start snapshot;
-    // adaptive, the state after the last accumulate on this batch's own stream (its retired bit
-    // included).  A pixel that retired in a batch still in flight is rendered speculatively and
-    // its samples are dropped by k_accumulate, in sample order, as in the serial schedule; a
-    // pixel that did not took every sample of those batches, so n + done is its next index.
-    // Serial calls read the live Stats.
+    // Concurrent fixed-spp calls take it from the call-start snapshot plus the samples of the
+    // batches before this one, so a batch never waits for the previous batch's accumulate.
+    // Serial and adaptive calls read the live Stats: an adaptive stream's pixels are its own, and
+    // its previous batch's accumulate has run on the same stream.
     uint32_t s;
     bool live;
     if (R.n0) {
@@ -339,10 +366,19 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
                                                  uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters,
                                                  const float2* __restrict__ hitbuf) {
     const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
-    uint32_t n;
+    uint32_t n, stride = R.n_pixels;
+    uint64_t first0 = seg0;                 // FIRST: the batch's first sample of this workgroup
     if (FIRST) {
-        const uint64_t paths = (uint64_t)R.n_pixels * R.batch;
-        n = seg0 < paths ? (uint32_t)std::min<uint64_t>(G.segcap, paths - seg0) : 0u;
+        uint64_t paths = (uint64_t)R.n_pixels * R.batch;
+        if (R.ad.list) {                    // adaptive: the stream's live list x the planned samples
+            const AdPlan pl = uniform_load(R.ad.plan);
+            stride = pl.c;
+            paths = (uint64_t)pl.c * ad_batch(pl.c, pl.done, R.ad.j, R.ad.A);
+            first0 = (uint64_t)blockIdx.x * seg_capacity(paths, G.nseg);
+            n = first0 < paths ? (uint32_t)std::min<uint64_t>(seg_capacity(paths, G.nseg), paths - first0) : 0u;
+        } else {
+            n = seg0 < paths ? (uint32_t)std::min<uint64_t>(G.segcap, paths - seg0) : 0u;
+        }
     } else {
         n = count_in[blockIdx.x];
     }
@@ -367,7 +403,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
             const uint64_t i = seg0 + jj;
             bool live = true;
             if (FIRST) {
-                live = gen_path(P, R, i, p, p_pixel, res_id);
+                live = gen_path(P, R, stride, first0 + jj, p, p_pixel, res_id);
             } else {
                 load_ray(in, i, p);
                 load_rest(in, i, p);       // issued before the trace: its latency hides behind it
@@ -428,8 +464,17 @@ template <bool COUNT>
 __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_raygen(OmParamsDev P, Seg G, Gen R, Queue out,
                                                  uint32_t* __restrict__ count_out, uint32_t* __restrict__ res_id) {
     const uint64_t seg0 = (uint64_t)blockIdx.x * G.segcap;
-    const uint64_t paths = (uint64_t)R.n_pixels * R.batch;
-    const uint32_t n = seg0 < paths ? (uint32_t)std::min<uint64_t>(G.segcap, paths - seg0) : 0u;
+    uint64_t paths = (uint64_t)R.n_pixels * R.batch, first0 = seg0;
+    uint32_t n, stride = R.n_pixels;
+    if (R.ad.list) {                        // adaptive: the stream's live list x the planned samples
+        const AdPlan pl = uniform_load(R.ad.plan);
+        stride = pl.c;
+        paths = (uint64_t)pl.c * ad_batch(pl.c, pl.done, R.ad.j, R.ad.A);
+        first0 = (uint64_t)blockIdx.x * seg_capacity(paths, G.nseg);
+        n = first0 < paths ? (uint32_t)std::min<uint64_t>(seg_capacity(paths, G.nseg), paths - first0) : 0u;
+    } else {
+        n = seg0 < paths ? (uint32_t)std::min<uint64_t>(G.segcap, paths - seg0) : 0u;
+    }
     __shared__ uint32_t q_out;
     if (threadIdx.x == 0) q_out = 0u;
     __syncthreads();
@@ -438,7 +483,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_raygen(OmParamsDev P, Se
         const uint32_t jj = base + threadIdx.x;
         Path p;
         uint32_t pixel;
-        const bool keep = jj < n && gen_path(P, R, seg0 + jj, p, pixel, res_id);
+        const bool keep = jj < n && gen_path(P, R, stride, first0 + jj, p, pixel, res_id);
         const uint64_t m = __ballot(keep);
         uint32_t obase = 0u;
         if (lane == 0 && m) obase = atomicAdd(&q_out, (uint32_t)__popcll(m));
@@ -602,8 +647,11 @@ __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const 
         }
         // march ended: handle_hit, next segment or done -- for the wave's ended lanes together, once
         // OM_WF_TAIL_SHADE of them wait or none marches
+        // (the ballots are taken before the branch, with every lane active: inside it only the
+        // ended lanes run, whose act is false, so a ballot of act there would always be 0)
         const bool ended = have && !act;
-        if (ended && (OM_WF_TAIL_SHADE <= 1 || __popcll(__ballot(ended)) >= OM_WF_TAIL_SHADE || __ballot(act) == 0)) {
+        const uint64_t em = __ballot(ended), am = __ballot(act);
+        if (ended && (OM_WF_TAIL_SHADE <= 1 || __popcll(em) >= OM_WF_TAIL_SHADE || am == 0)) {
             if (COUNT) segs++;
             unpark();
             if (shade_path<true>(S, P, depth_cap, p, closest, best, res, res_id)) begin();
@@ -683,15 +731,30 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmPar
 }
 
 // ---------------------------------------------------------------- accumulate
+// Adaptive batches (ad.list): lane kk owns live-list entry kk, and a pixel that is still live after
+// the batch, with samples of the call left, is appended to the stream's next list (one ballot and
+// one atomic per wave: ThreadPixels::add_run / swap_buffers, render_thread.rs:68-102).  The list's
+// order then depends on which wave appends first; a result's slot and a path's RNG never do.
 template <bool COUNT>
 __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_stats* __restrict__ stats,
                                                      const uint32_t* __restrict__ pixels, uint32_t n_pixels, uint32_t by_pixel,
                                                      uint32_t batch, const float4* __restrict__ res,
                                                      const uint32_t* __restrict__ res_id, const uint64_t* __restrict__ bloom,
-                                                     uint32_t* __restrict__ snap, unsigned long long* __restrict__ counters) {
-    const uint32_t k = blockIdx.x * kBlk + threadIdx.x;
+                                                     AdList ad, unsigned long long* __restrict__ counters) {
+    const uint32_t kk = blockIdx.x * kBlk + threadIdx.x;
     uint32_t n_samples = 0, credited = 0;
-    if (k < n_pixels) {
+    uint32_t done0 = 0;
+    if (ad.list) {
+        const AdPlan pl = uniform_load(ad.plan);
+        n_pixels = pl.c;
+        batch = ad_batch(pl.c, pl.done, ad.j, ad.A);
+        done0 = pl.done;
+        if (kk == 0) ad.plan_next->done = pl.done + batch;
+    }
+    bool relist = false;
+    uint32_t k = kk;
+    if (kk < n_pixels) {
+        if (ad.list) k = ad.list[kk];
         const uint32_t slot = by_pixel ? pixels[k] : k;
         const om_pixel_stats in = stats[slot];
         PixelState st;
@@ -708,10 +771,10 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
             float4 rr[OM_ACC_GROUP];
             uint64_t bl[OM_ACC_GROUP];
 #pragma unroll
-            for (uint32_t j = 0; j < OM_ACC_GROUP; ++j) id[j] = j < m ? res_id[(uint64_t)(s0 + j) * n_pixels + k] : kNoSample;
+            for (uint32_t j = 0; j < OM_ACC_GROUP; ++j) id[j] = j < m ? res_id[(uint64_t)(s0 + j) * n_pixels + kk] : kNoSample;
 #pragma unroll
             for (uint32_t j = 0; j < OM_ACC_GROUP; ++j) {
-                if (j < m) rr[j] = res[(uint64_t)(s0 + j) * n_pixels + k];
+                if (j < m) rr[j] = res[(uint64_t)(s0 + j) * n_pixels + kk];
                 bl[j] = bloom[id[j] == kNoSample ? 0u : id[j]];
             }
 #pragma unroll
@@ -733,7 +796,14 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
         out.color[0] = (uint8_t)(st.rgbf & 0xFFu); out.color[1] = (uint8_t)((st.rgbf >> 8) & 0xFFu);
         out.color[2] = (uint8_t)((st.rgbf >> 16) & 0xFFu); out.flags = (uint8_t)(st.rgbf >> 24); out.reserved = 0u;
         stats[slot] = out;
-        if (snap) snap[k] = st.n | ((st.rgbf >> 24) & 1u) << 31;   // concurrent adaptive calls (Gen::n0)
+        relist = ad.list && !(st.rgbf & 0x01000000u) && st.n < P.spp_total && done0 + batch < ad.A.sample_count;
+    }
+    if (ad.list) {                                                  // the stream's next live list
+        const uint64_t m = __ballot(relist);
+        uint32_t base = 0u;
+        if (__lane_id() == 0 && m) base = atomicAdd(&ad.plan_next->c, (uint32_t)__popcll(m));
+        base = __builtin_amdgcn_readfirstlane(base);
+        if (relist) ad.list_next[base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull))] = k;
     }
     if (COUNT) {
         flush_counter(counters, OMC_SAMPLES, n_samples);
@@ -742,16 +812,34 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
     if (P.progress) flush_counter(counters, OMC_PROGRESS, credited);      // live samples_atom (om_progress)
 }
 
-// k_snapshot: n0[c * n_pixels + k] = Stats.n of listed pixel k at the start of a concurrent
-// call (| retired << 31 in adaptive calls), for each of `copies` streams.
+// k_snapshot: n0[k] = Stats.n of listed pixel k at the start of a concurrent fixed-spp call.
 __global__ __launch_bounds__(256) void k_snapshot(const om_pixel_stats* __restrict__ stats, const uint32_t* __restrict__ pixels,
-                                                  uint32_t n_pixels, uint32_t by_pixel, uint32_t adaptive, uint32_t copies,
-                                                  uint32_t* __restrict__ n0) {
+                                                  uint32_t n_pixels, uint32_t by_pixel, uint32_t* __restrict__ n0) {
     const uint32_t k = blockIdx.x * 256u + threadIdx.x;
     if (k >= n_pixels) return;
-    const om_pixel_stats& ps = stats[by_pixel ? pixels[k] : k];
-    const uint32_t v = ps.n | ((adaptive && (ps.flags & 1u)) ? 0x80000000u : 0u);
-    for (uint32_t c = 0; c < copies; ++c) n0[(uint64_t)c * n_pixels + k] = v;
+    n0[k] = stats[by_pixel ? pixels[k] : k].n;
+}
+
+// k_ad_init: the first live list of every stream of an adaptive call.  Chunk q of 64 list entries
+// (a tile of a frame list) belongs to stream q % ns; its pixels that are not retired and have
+// samples left are appended to that stream's list (one ballot + one atomic per wave: a wave is one
+// chunk).  plans (zeroed by the caller) get the counts.
+__global__ __launch_bounds__(256) void k_ad_init(const om_pixel_stats* __restrict__ stats, const uint32_t* __restrict__ pixels,
+                                                 uint32_t n_pixels, uint32_t by_pixel, uint32_t spp_total, uint32_t ns,
+                                                 uint32_t* __restrict__ lists, uint64_t list_stride, AdPlan* __restrict__ plans,
+                                                 uint32_t plan_stride) {
+    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    bool live = false;
+    if (k < n_pixels) {
+        const om_pixel_stats& ps = stats[by_pixel ? pixels[k] : k];
+        live = !(ps.flags & 1u) && ps.n < spp_total;
+    }
+    const uint32_t s = (k >> 6) % ns;                                // wave-uniform
+    const uint64_t m = __ballot(live);
+    uint32_t base = 0u;
+    if (__lane_id() == 0 && m) base = atomicAdd(&plans[(uint64_t)s * plan_stride].c, (uint32_t)__popcll(m));
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (live) lists[s * list_stride + base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull))] = k;
 }
 
 hipError_t grow(Buffers& B, uint64_t cap, uint32_t counts_n, int nsets) {
@@ -878,56 +966,69 @@ hipError_t ensure_events(Buffers& B, size_t n) {
 
 }  // namespace
 
-// Schedules (DESIGN.md §5.5):
-//   serial      (L.streams == 1) one batch after another on `st`; an adaptive batch's bounce 0
-//               reads the Stats its predecessor's accumulate wrote.
-//   concurrent  (default) the call's samples split into batches of at most half
-//               the call, dealt round-robin to L.streams streams (`st` + side streams), each
-//               with its own queue set: two batches are in flight at once, so one batch's
-//               latency-bound phases (the drain of every launch, the late bounces, the tail)
-//               run beside the other's full ones.  Accumulates stay in sample order through
-//               events (acc i after acc i-1) and the call ends joined on `st`.  Sample indices
-//               come from Stats.n snapshots (n0: the call start's, or for adaptive calls the
-//               state after the stream's previous batch), so every schedule renders identical
-//               bits; an adaptive batch renders the pixels that retire in the batch running
-//               beside it speculatively, and k_accumulate drops those samples.
+// Schedules (DESIGN.md §5.5, §5.8):
+//   fixed spp, serial      (L.streams == 1) one batch after another on `st`.
+//   fixed spp, concurrent  (default) the call's samples split into batches of at most half the
+//               call, dealt round-robin to L.streams streams (`st` + side streams), each with its
+//               own queue set: two batches are in flight at once, so one batch's latency-bound
+//               phases (the drain of every launch, the late bounces, the tail) run beside the
+//               other's full ones.  Sample indices come from the call-start Stats.n snapshot (n0).
+//   adaptive    the listed pixels are dealt to the streams by 64-entry chunks; each stream runs
+//               up to ad_batches batches over ITS live pixels, from a live list its own
+//               k_accumulate compacts, with the batch's sample count planned on the device from
+//               the live count (ad_batch): nothing is rendered for a retired pixel, and samples
+//               past a retirement inside a batch are dropped in sample order by k_accumulate.
+// In both concurrent forms the accumulates run in batch order through events (acc i after
+// acc i-1) and the call ends joined on `st`.
 // Timing: mode 2 brackets the call once on `st` (OM_KT_BOUNCE_SPAN, with the call's
 // bounce-family launch count); mode 1 brackets every launch on its stream and the call.
 hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err) {
     const uint32_t n_px = L.n_pixels;
     if (n_px == 0 || L.P.sample_count == 0) return hipSuccess;
-    // paths per batch: 2^25 (33.5M, ~4.9 GB of queues per set; 16 spp of 1080p, the measured sweet
-    // spot, §5.5), raised up to 16 spp of the frame for frames above 2M pixels, within 2^27 (~21 GB
-    // per set, two sets; MI355X has 288 GB): a 4K frame (C4, 8.3M pixels) then runs 16-spp batches
-    // like 1080p instead of 4-spp ones, whose 4x launches and 4x Stats read-modify-write per sample
-    // cost C4 ~11% in k_accumulate alone (r03)
+    const bool adaptive = L.P.adaptive != 0u;
+    const uint32_t want = std::max<uint32_t>(1u, std::min<uint32_t>(L.streams, (uint32_t)kMaxSets));
+    // fixed spp: paths per batch 2^25 (33.5M, ~4.9 GB of queues per set; 16 spp of 1080p, the
+    // measured sweet spot, §5.5), raised up to 16 spp of the frame for frames above 2M pixels,
+    // within 2^27 (~21 GB per set, two sets; MI355X has 288 GB): a 4K frame (C4, 8.3M pixels) then
+    // runs 16-spp batches like 1080p instead of 4-spp ones, whose 4x launches and 4x Stats
+    // read-modify-write per sample cost C4 ~11% in k_accumulate alone (r03)
     const uint64_t kMaxPaths = std::min<uint64_t>(1ull << OM_WF_MAX_PATHS_LOG2,
                                                   std::max<uint64_t>(1ull << OM_WF_MIN_PATHS_LOG2, (uint64_t)OM_WF_BATCH_SPP * n_px));
-    const uint32_t want = std::max<uint32_t>(1u, std::min<uint32_t>(L.streams, (uint32_t)kMaxSets));
-    const bool concurrent = want >= 2u && L.P.sample_count >= 2u;
-    uint32_t batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));
-    if (L.P.adaptive) batch = std::min<uint32_t>(batch, OM_WF_ADAPTIVE_BATCH);
-    // fixed spp: at most 1/want of the call per batch, so every call has batches in flight
-    // together; adaptive: full 16-sample batches (a call of 16 samples runs as one), and the
-    // call's later batches OM_WF_ADAPTIVE_BATCH_LATER samples (within 2^OM_WF_MAX_PATHS_LOG2 paths):
-    // by then most pixels have retired, so a batch's live paths are few
-    if (concurrent && !L.P.adaptive) batch = std::min<uint32_t>(batch, (L.P.sample_count + want - 1u) / want);
-    const uint32_t later = L.P.adaptive
-        ? (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)OM_WF_ADAPTIVE_BATCH_LATER,
-                                                             (1ull << OM_WF_MAX_PATHS_LOG2) / n_px))
-        : batch;
-    std::vector<uint32_t> done_at(1, 0u);                          // samples of the call before batch i
-    while (done_at.back() < L.P.sample_count)
-        done_at.push_back(done_at.back() + std::min(done_at.size() == 1 ? batch : later, L.P.sample_count - done_at.back()));
-    const uint32_t nb = (uint32_t)done_at.size() - 1u;
-    const uint32_t bmax = std::max(batch, nb > 1 ? later : 0u);
-    const uint32_t ns = concurrent ? std::min<uint32_t>(want, nb) : 1u;
+    uint32_t ns, nb, batch = 0, ad_k = 0, cmax = 0;
+    uint64_t max_paths;
+    std::vector<uint32_t> done_at(1, 0u);                          // fixed spp: samples of the call before batch i
+    AdCfg A{};
+    if (adaptive) {
+        const uint32_t chunks = (n_px + 63u) / 64u;
+        ns = std::min<uint32_t>(want, chunks);
+        cmax = std::min<uint32_t>(n_px, (chunks + ns - 1u) / ns * 64u);   // entries of the fullest stream
+        // batches per stream: OM_WF_ADAPTIVE_BATCHES, more when the forced even share of a large
+        // call would exceed 2^OM_WF_ADAPTIVE_CAP_LOG2 paths
+        const uint64_t capmax = 1ull << OM_WF_ADAPTIVE_CAP_LOG2;
+        uint64_t k = L.ad_batches ? L.ad_batches : OM_WF_ADAPTIVE_BATCHES;
+        while (k < L.P.sample_count && (uint64_t)cmax * ((L.P.sample_count + k - 1u) / k) > capmax) ++k;
+        ad_k = (uint32_t)std::min<uint64_t>(k, L.P.sample_count);
+        A.sample_count = L.P.sample_count; A.batches = ad_k;
+        A.paths = 1u << (L.ad_paths_log2 ? L.ad_paths_log2 : OM_WF_ADAPTIVE_PATHS_LOG2);
+        max_paths = std::max<uint64_t>(std::min<uint64_t>(A.paths, (uint64_t)cmax * L.P.sample_count),
+                                       (uint64_t)cmax * ((L.P.sample_count + ad_k - 1u) / ad_k));
+        nb = ad_k * ns;
+    } else {
+        const bool concurrent = want >= 2u && L.P.sample_count >= 2u;
+        batch = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(L.P.sample_count, kMaxPaths / n_px));
+        // at most 1/want of the call per batch, so every call has batches in flight together
+        if (concurrent) batch = std::min<uint32_t>(batch, (L.P.sample_count + want - 1u) / want);
+        while (done_at.back() < L.P.sample_count)
+            done_at.push_back(done_at.back() + std::min(batch, L.P.sample_count - done_at.back()));
+        nb = (uint32_t)done_at.size() - 1u;
+        ns = concurrent ? std::min<uint32_t>(want, nb) : 1u;
+        max_paths = (uint64_t)n_px * batch;
+    }
     const uint32_t depth_cap = L.P.max_depth > 1u ? L.P.max_depth : 1u;
     int dev = 0;
     (void)hipGetDevice(&dev);
     int cus = 256;
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const uint64_t max_paths = (uint64_t)n_px * bmax;
     int tr = L.trace_mode == TR_SBVH_LDS ? TR_SBVH_GLOBAL : L.trace_mode;
     if (tr == TR_BVH4_LDS) tr = L.S.n_b4nodes == 0 ? TR_BVH2_LDS : (L.S.b4_lds_bytes ? TR_BVH4_LDS : TR_BVH4_GLOBAL);
     // an empty BVH2 (no bounded sphere/cube: marched-only worlds, C2) takes the reference loop
@@ -940,7 +1041,8 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
     const uint32_t tail_at = L.tail_bounce ? L.tail_bounce
                            : march ? kTailMarched : tr == TR_BVH2_GLOBAL ? kTailL2
-                           : (uint64_t)n_px * batch > (1ull << 25) ? kTailBigBatch : kTailDefault;
+                           : adaptive ? OM_WF_ADAPTIVE_TAIL
+                           : max_paths > (1ull << 25) ? kTailBigBatch : kTailDefault;
     const uint32_t lanes_per_cu = (march || tr == TR_BVH2_GLOBAL) ? OM_WF_LANES_PER_CU_WIDE : OM_WF_LANES_PER_CU;
     uint32_t nseg = (uint32_t)std::min<uint64_t>((max_paths + kBlk - 1) / kBlk, (uint64_t)cus * (lanes_per_cu / kBlk));
     nseg = (nseg + kTailSpb - 1) / kTailSpb * kTailSpb;
@@ -955,24 +1057,28 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     R.C = L.C; R.jitter = L.jitter; R.stats = L.stats; R.pixels = L.pixels; R.n_pixels = n_px;
     R.by_pixel = L.stats_by_pixel ? 1u : 0u;
     R.tile_off = L.tile_off; R.tile_idx = L.tile_idx; R.tile_tnear = L.tile_tnear;
-    R.n0 = nullptr; R.done = 0;
+    R.n0 = nullptr; R.done = 0; R.ad = AdList{};
     hipStream_t streams[kMaxSets] = {st, st, st, st};
     Timer& tm = *L.timer;
     const int call_ti = tm.begin(st);
-    // snapshots (Gen::n0): fixed spp, one of the call start; concurrent adaptive, one per stream,
-    // rewritten by every accumulate on that stream.  Serial adaptive calls read the live Stats.
-    const bool adaptive_snaps = L.P.adaptive && concurrent;
-    const uint32_t copies = adaptive_snaps ? ns : 1u;
-    if (!L.P.adaptive || adaptive_snaps) {
-        const uint64_t need = (uint64_t)n_px * copies;
-        if (need > B.n0_cap) {
-            if (B.n0) (void)hipFree(B.n0);
-            B.n0 = nullptr; B.n0_cap = 0;
-            if ((e = hipMalloc(&B.n0, (size_t)need * sizeof(uint32_t))) != hipSuccess) { err = "n0 allocation failed"; return e; }
-            B.n0_cap = need;
-        }
-        hipLaunchKernelGGL(k_snapshot, dim3((n_px + 255u) / 256u), dim3(256), 0, st, L.stats, L.pixels, n_px,
-                           R.by_pixel, L.P.adaptive ? 1u : 0u, copies, B.n0);
+    // device words: fixed spp, the call-start Stats.n snapshot (n0, concurrent calls); adaptive, per
+    // stream two live lists (ping-pong) of cmax entries and ad_k + 1 plans
+    const uint32_t plan_stride = ad_k + 1u;
+    const uint64_t words = adaptive ? (uint64_t)ns * 2u * cmax + (uint64_t)ns * plan_stride * 2u : (ns > 1 ? n_px : 0u);
+    if (words > B.n0_cap) {
+        if (B.n0) (void)hipFree(B.n0);
+        B.n0 = nullptr; B.n0_cap = 0;
+        if ((e = hipMalloc(&B.n0, (size_t)words * sizeof(uint32_t))) != hipSuccess) { err = "n0 allocation failed"; return e; }
+        B.n0_cap = words;
+    }
+    uint32_t* lists = B.n0;
+    AdPlan* plans = adaptive ? (AdPlan*)(B.n0 + (uint64_t)ns * 2u * cmax) : nullptr;
+    if (adaptive) {
+        (void)hipMemsetAsync(plans, 0, (size_t)ns * plan_stride * sizeof(AdPlan), st);
+        hipLaunchKernelGGL(k_ad_init, dim3((n_px + 255u) / 256u), dim3(256), 0, st, L.stats, L.pixels, n_px, R.by_pixel,
+                           L.P.spp_total, ns, lists, (uint64_t)2u * cmax, plans, plan_stride);
+    } else if (ns > 1) {
+        hipLaunchKernelGGL(k_snapshot, dim3((n_px + 255u) / 256u), dim3(256), 0, st, L.stats, L.pixels, n_px, R.by_pixel, B.n0);
         R.n0 = B.n0;
     }
     // events: [0] call start on `st`, [k] side stream k joined, [kMaxSets + i] batch i accumulated
@@ -989,23 +1095,33 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     }
     uint32_t launches = 0;
     for (uint32_t i = 0; i < nb; ++i) {
-        const uint32_t done = done_at[i], b = done_at[i + 1] - done;
-        const uint64_t paths = (uint64_t)n_px * b;
-        hipStream_t si = streams[i % ns];
-        QueueSet& QS = B.set[i % ns];
+        const uint32_t sidx = i % ns;                             // stream (and queue set) of batch i
+        hipStream_t si = streams[sidx];
+        QueueSet& QS = B.set[sidx];
         Seg G;
         G.nseg = nseg;
-        G.segcap = seg_capacity(paths, nseg);
-        R.batch = b;
-        R.done = done;
-        uint32_t* snap = nullptr;
-        if (adaptive_snaps) {
-            // batch i reads the snapshot its stream's last accumulate (batch i - ns) wrote, i.e. the
-            // state after batch i - ns; batches i - ns + 1 .. i - 1 (all full) lie between
-            snap = B.n0 + (uint64_t)(i % ns) * n_px;
-            R.n0 = snap;
-            R.done = i >= ns ? done - done_at[i - ns + 1u] : done;
+        uint32_t b = 0, grid_a;
+        AdList ad{};
+        if (adaptive) {
+            // batch j of stream sidx: its live list and plan, the next ones written by its accumulate
+            const uint32_t j = i / ns;
+            uint32_t* lbase = lists + (uint64_t)sidx * 2u * cmax;
+            ad.list = lbase + (uint64_t)(j & 1u) * cmax;
+            ad.list_next = lbase + (uint64_t)((j + 1u) & 1u) * cmax;
+            ad.plan = plans + (uint64_t)sidx * plan_stride + j;
+            ad.plan_next = plans + (uint64_t)sidx * plan_stride + j + 1u;
+            ad.A = A; ad.j = j;
+            G.segcap = segcap;                                    // queue capacity of the largest batch
+            grid_a = (cmax + kBlk - 1) / kBlk;
+        } else {
+            const uint32_t done = done_at[i];
+            b = done_at[i + 1] - done;
+            G.segcap = seg_capacity((uint64_t)n_px * b, nseg);
+            R.done = done;
+            grid_a = (n_px + kBlk - 1) / kBlk;
         }
+        R.batch = b;
+        R.ad = ad;
         switch (tr) {
             case TR_BRUTE: launches += run_tr<TR_BRUTE>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
             case TR_CULLED: launches += run_tr<TR_CULLED>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
@@ -1016,15 +1132,17 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
             case TR_BVH4_GLOBAL: launches += run_tr<TR_BVH4_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
             default: launches += run_tr<TR_BVH2_GLOBAL>(L.count, march, QS, L, si, G, R, depth_cap, tail_at, lds); break;
         }
-        if (ns > 1 && i > 0) (void)hipStreamWaitEvent(si, B.ev[kMaxSets + i - 1u], 0);   // Stats::add in sample order
-        const uint32_t grid_a = (n_px + kBlk - 1) / kBlk;
+        // accumulates in batch order: fixed spp needs it (Stats::add in sample order); an adaptive
+        // stream's pixels are its own, so there it only keeps the streams in step and the progress
+        // copies in order (unchained streams measured the same: 49.3 vs 49.2 ms per frame, r05_p6)
+        if (ns > 1 && i > 0) (void)hipStreamWaitEvent(si, B.ev[kMaxSets + i - 1u], 0);
         const int ati = tm.mode == 1 ? tm.begin(si) : -1;
         if (L.count)
             hipLaunchKernelGGL(k_accumulate<true>, dim3(grid_a), dim3(kBlk), 0, si, L.P, L.stats, L.pixels, n_px,
-                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, snap, L.counters);
+                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, ad, L.counters);
         else
             hipLaunchKernelGGL(k_accumulate<false>, dim3(grid_a), dim3(kBlk), 0, si, L.P, L.stats, L.pixels, n_px,
-                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, snap, L.counters);
+                               L.stats_by_pixel ? 1u : 0u, b, QS.res, QS.res_id, L.S.bloom, ad, L.counters);
         tm.end(ati, OM_KT_ACCUMULATE, si);
         // live progress: the cumulative credit after this batch, to the host word om_progress
         // hands out; ahead of the event the next batch's accumulate waits on, so the copies

@@ -120,7 +120,7 @@ def test_adaptive_retirement_bit_exact(om, oracle, pipeline):
 
 @pytest.mark.parametrize("sample_count", [1, 5, 24])
 def test_adaptive_speculative_batches_bit_exact(om, oracle, sample_count):
-    """Wavefront adaptive calls render up to 16 samples per pixel per batch and drop those
+    """Wavefront adaptive calls render several samples per live pixel per batch and drop those
     past a pixel's retirement: progressive calls of 1 / 5 / 24 samples ==
     the sequential oracle, on a frame bigger than one workgroup's segment."""
     W, H, SPP = 72, 40, 24
@@ -349,13 +349,14 @@ def test_concurrent_batches_are_bit_identical(om, oracle, streams):
 
 
 @pytest.mark.parametrize("streams", [1, 2, 3, 4])
-def test_concurrent_adaptive_batches_are_bit_identical(om, oracle, streams):
-    """Adaptive calls split into batches in flight on 1-4 streams: each batch
-    takes its sample indices and retired bits from the snapshot its stream's previous accumulate
-    wrote, renders the pixels that retire in the batches beside it speculatively, and
-    k_accumulate drops those samples in sample order.  Calls of 7, 16 and 17 samples (one to
-    four batches per call) and a 40-sample call (batches past the first `streams`, which read
-    a snapshot written inside the call) == the sequential oracle."""
+@pytest.mark.parametrize("sched", [(0, 0), (2, 10), (7, 8)])
+def test_concurrent_adaptive_batches_are_bit_identical(om, oracle, streams, sched):
+    """Adaptive calls on 1-4 streams: the live pixels dealt to the streams by
+    64-entry chunks, each stream's batches planned on the device from its live list (compacted by
+    every accumulate), samples past a retirement inside a batch dropped in sample order.  Schedules
+    (om_set_adaptive_batches): the default; at most 2 batches per stream per call with 2^10 paths
+    targeted (the even share of the call decides); 7 batches at 2^8 paths (every batch of a stream
+    sized by its live count).  Calls of 7, 16 and 17 samples and one of 40 == the sequential oracle."""
     from raytracingoneweekend_amd import _lib as L
     W, H, SPP = 72, 40, 40
     world = om.random_scene(0x5EED)
@@ -365,12 +366,36 @@ def test_concurrent_adaptive_batches_are_bit_identical(om, oracle, streams):
     for counts in ((7, 16, 17), (40,)):
         fz = world.freeze(cam, kernel="auto", pipeline="wavefront")
         L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
+        L.check(L.lib.om_set_adaptive_batches(fz.ctx, *sched), fz.ctx)
         pix = om.PixelsBox.new(W * H)
         for c in counts:
             om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=21, adaptive=True, sample_count=c)
-        nb, msg = compare_stats(pix.pixels, exp, f"adaptive streams{streams} calls{counts}")
+        nb, msg = compare_stats(pix.pixels, exp, f"adaptive streams{streams} sched{sched} calls{counts}")
         assert nb == 0, msg
         assert int(pix.pixels["n"].min()) < SPP
+    assert L.lib.om_set_adaptive_batches(fz.ctx, 5000, 0) == L.OM_ERR_INVALID
+    assert L.lib.om_set_adaptive_batches(fz.ctx, 0, 28) == L.OM_ERR_INVALID
+
+
+@pytest.mark.parametrize("streams", [1, 2, 3])
+def test_concurrent_adaptive_marched_bit_identical(om, oracle, streams):
+    """The adaptive schedule on a marched world: camera paths through k_raygen's live
+    list, the lane-refilling tail from bounce 1, several batches per stream (2^8 paths targeted),
+    calls of 17 and 40 samples == the sequential oracle."""
+    from raytracingoneweekend_amd import _lib as L
+    W, H, SPP = 40, 24, 57
+    exp, _ = oracle.render(oracle.marched_scene(), oracle.default_camera(W / H),
+                           oracle.params(W, H, SPP, seed=23, adaptive=True, march_steps=256))
+    cam = om.default_camera(W / H)
+    fz = om.marched_scene().freeze(cam, pipeline="wavefront")
+    L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
+    L.check(L.lib.om_set_adaptive_batches(fz.ctx, 6, 8), fz.ctx)
+    pix = om.PixelsBox.new(W * H)
+    for c in (17, 40):
+        om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=23, adaptive=True, sample_count=c, march_steps=256)
+    nb, msg = compare_stats(pix.pixels, exp, f"adaptive marched streams{streams}")
+    assert nb == 0, msg
+    assert int(pix.pixels["n"].min()) < SPP
 
 
 @pytest.mark.parametrize("pipeline", PIPELINES)

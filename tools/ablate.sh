@@ -58,12 +58,8 @@ declare -A V=(
   [trf32]="$COMMON $DEV -DOM_WF_TAIL_REFILL=32"
   [mu4]="$COMMON $DEV -DOM_MARCH_UNROLL=4"
   [mu12]="$COMMON $DEV -DOM_MARCH_UNROLL=12"
-  # adaptive wavefront: samples per pixel per serial batch
-  [ab4]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=4"
-  [ab8]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH=8"
-  [al16]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH_LATER=16"
-  [al32]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH_LATER=32"
-  [al64]="$COMMON $DEV -DOM_WF_ADAPTIVE_BATCH_LATER=64"
+  # adaptive wavefront: tail threshold of adaptive batches
+  [adt16]="$COMMON $DEV -DOM_WF_ADAPTIVE_TAIL=16"
   # batch shape: 2^25 paths for every frame (C4 in 4-spp batches), 8 / 32-spp batches
   [mp25]="$COMMON $DEV -DOM_WF_MAX_PATHS_LOG2=25"
   [bs8]="$COMMON $DEV -DOM_WF_BATCH_SPP=8 -DOM_WF_MIN_PATHS_LOG2=20"

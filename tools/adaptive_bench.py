@@ -33,10 +33,18 @@ def main():
     out = {"frame": f"{scene} {W}x{H}, {SPP} spp adaptive, {STEP} spp per call"}
     frames = {}
     extra = [int(x) for x in sys.argv[4].split(",")] if len(sys.argv) > 4 else []   # more stream counts
-    for name, pipe, streams in ([("wavefront", "wavefront", 2), ("wavefront_serial", "wavefront", 1),
-                                 ("megakernel", "megakernel", 1)] + [(f"wavefront_s{k}", "wavefront", k) for k in extra]):
+    # AD_SCHEDS="K,P;K,P": more wavefront runs with om_set_adaptive_batches(K, P) (2 streams)
+    scheds = [tuple(int(v) for v in x.split(",")) for x in os.environ.get("AD_SCHEDS", "").split(";") if x]
+    runs = ([("wavefront", "wavefront", 2, (0, 0))]
+            + ([] if os.environ.get("AD_NO_SERIAL") else [("wavefront_serial", "wavefront", 1, (0, 0))])
+            + ([] if os.environ.get("AD_NO_MEGA") else [("megakernel", "megakernel", 1, (0, 0))])
+            + [(f"wavefront_s{k}", "wavefront", k, (0, 0)) for k in extra]
+            + [(f"wavefront_k{a}_p{b}", "wavefront", 2, (a, b)) for a, b in scheds])
+    for name, pipe, streams, sched in runs:
         fz = world.freeze(cam, pipeline=pipe)
         L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
+        L.check(L.lib.om_set_adaptive_batches(fz.ctx, *sched), fz.ctx)
+        L.check(L.lib.om_set_tail_bounce(fz.ctx, int(os.environ.get("AD_TAIL", "0"))), fz.ctx)
         st = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
         p = om.make_params(50, 0.001, 100.0, SPP, W, H, sample_count=STEP, seed=1, adaptive=True,
                            march_steps=256)
@@ -67,7 +75,8 @@ def main():
         frames[name] = st.cpu()
         out[name] = {"s": round(dt, 4), "frames_s": [round(x, 4) for x in reps], "taken_msamples_s": round(ctr.samples / dt / 1e6, 1),
                      "credited_msamples_s": round(ctr.credited / dt / 1e6, 1),
-                     "taken_frac": round(ctr.samples / (W * H * SPP), 4)}
+                     "taken_frac": round(ctr.samples / (W * H * SPP), 4),
+                     "segments_g": round(ctr.segments / 1e9, 4), "gseg_s": round(ctr.segments / dt / 1e9, 2)}
     out["schedules_bit_identical"] = all(bool(torch.equal(frames["wavefront"], f)) for f in frames.values())
     print(json.dumps(out))
 

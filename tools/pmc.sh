@@ -9,6 +9,10 @@ TAG=${1:-pmc}; shift
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 ARGS="--steps 4 --warmup 1 --no-cpu-baseline --no-window-parity $*"
+# PMC_CMD: another program to profile (e.g. the adaptive frame, tools/adaptive_bench.py)
+CMD=${PMC_CMD:-"python bench.py $ARGS"}
+# the build the passes profile (om_build_id), for bench.py's pmc fields (pmc_summary.py reads it)
+python -c "from raytracingoneweekend_amd import _lib as L; print(L.build_id())" > "$OUT/build_id.txt" || exit 1
 i=0
 for PASS in "SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS" \
             "SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU_FLOPS_FP32 SQ_LDS_BANK_CONFLICT SQ_INSTS_BRANCH SQ_WAIT_INST_LDS SQ_INSTS_VMEM" \
@@ -16,6 +20,6 @@ for PASS in "SQ_WAVES SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ
   i=$((i+1))
   case " ${PASSES:-1 2 3 4 5} " in *" $i "*) ;; *) continue ;; esac
   timeout -k 10 300 rocprofv3 --kernel-trace --pmc $PASS -d "$OUT/p$i" -o run --output-format csv -- \
-      python bench.py $ARGS > "$OUT/p$i.log" 2>&1 || { echo "pmc pass $i failed"; exit 1; }
+      $CMD > "$OUT/p$i.log" 2>&1 || { echo "pmc pass $i failed"; exit 1; }
 done
 echo ok

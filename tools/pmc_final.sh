@@ -1,7 +1,8 @@
 #!/bin/bash
 # End-of-round PMC passes (GPU box), summarised on the box so gpurun_out/ stays small:
 #   C1 all five passes -> pmc_summary_C1.json + pmc_traffic.json; C2 all five -> *_C2.json;
-#   C3 all five -> *_C3.json; C4 the FETCH_SIZE / WRITE_SIZE passes -> pmc_traffic_C4.json.
+#   C3 all five -> *_C3.json; C4 all five -> *_C4.json; C1_adaptive (the bench's adaptive frame,
+#   tools/adaptive_bench.py, concurrent schedule only) all five -> *_C1_adaptive.json.
 #   Raw pass files are deleted.
 #   [CONFIGS="C1 C2 C3 C4"] bash tools/pmc_final.sh TAG      -> gpurun_out/TAG/pmc_*.json
 set -o pipefail
@@ -18,8 +19,11 @@ run() {   # name, passes, bench args...
   python tools/pmc_traffic.py "$OUT/raw_$name" "$OUT/pmc_traffic_$name.json" || return 1
   rm -rf "$OUT/raw_$name"
 }
-case " ${CONFIGS:-C1 C2 C3 C4} " in *" C1 "*) run C1 "1 2 3 4 5" --no-extras || exit 1 ;; esac
-case " ${CONFIGS:-C1 C2 C3 C4} " in *" C2 "*) run C2 "1 2 3 4 5" --config C2 --no-extras || exit 1 ;; esac
-case " ${CONFIGS:-C1 C2 C3 C4} " in *" C3 "*) run C3 "1 2 3 4 5" --config C3 --no-extras || exit 1 ;; esac
-case " ${CONFIGS:-C1 C2 C3 C4} " in *" C4 "*) run C4 "3 4" --config C4 --no-extras || exit 1 ;; esac
+case " ${CONFIGS:-C1 C2 C3 C4 C1_adaptive} " in *" C1 "*) run C1 "1 2 3 4 5" --no-extras || exit 1 ;; esac
+case " ${CONFIGS:-C1 C2 C3 C4 C1_adaptive} " in *" C2 "*) run C2 "1 2 3 4 5" --config C2 --no-extras || exit 1 ;; esac
+case " ${CONFIGS:-C1 C2 C3 C4 C1_adaptive} " in *" C3 "*) run C3 "1 2 3 4 5" --config C3 --no-extras || exit 1 ;; esac
+case " ${CONFIGS:-C1 C2 C3 C4 C1_adaptive} " in *" C4 "*) run C4 "1 2 3 4 5" --config C4 --no-extras || exit 1 ;; esac
+case " ${CONFIGS:-C1 C2 C3 C4 C1_adaptive} " in *" C1_adaptive "*)
+  export AD_NO_SERIAL=1 AD_NO_MEGA=1 PMC_CMD="python tools/adaptive_bench.py 128 C1 512"
+  run C1_adaptive "1 2 3 4 5" || exit 1; unset PMC_CMD ;; esac
 echo ok

@@ -82,7 +82,9 @@ def summarise(tag, pattern):
             tot[c] += sum(v)
             cnt[c] += len(v)
     comb = {c: tot[c] / cnt[c] for c in tot}
-    return {"kernel_regex": pattern, "source": tag, "kernels": kernels,
+    bid = os.path.join(tag, "build_id.txt")                 # written by tools/pmc.sh: the profiled library
+    build = open(bid).read().strip() if os.path.exists(bid) else None
+    return {"kernel_regex": pattern, "source": tag, "build_id": build, "kernels": kernels,
             "combined": {"dispatches": dict(cnt), "counters": comb, "derived": derived(comb)}}
 
 
