@@ -151,6 +151,8 @@ struct Builder {
     }
 };
 
+}  // namespace
+
 // IEEE half bits -> the value, exactly (every half is a float).
 float half_value(uint16_t h) {
     const int e = (h >> 10) & 31, m = h & 1023;
@@ -173,7 +175,6 @@ uint16_t half_out(float x, bool up) {
     return bits(lo);
 }
 
-}  // namespace
 
 void build_bvh(const om_world& w, FrozenWorld& fw) {
     Builder b;

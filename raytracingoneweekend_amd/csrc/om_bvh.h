@@ -10,5 +10,10 @@
 
 namespace om {
 void build_bvh(const om_world& w, FrozenWorld& fw);
+// the half-precision node planes (OmBvh2NodeH): a half's exact value, and the half that holds a
+// float plane on the outside (lo: the largest half <= x, hi: the smallest half >= x; NaN -> the
+// infinite plane, so a NaN box culls nothing)
+float half_value(uint16_t h);
+uint16_t half_out(float x, bool up);
 void build_skip_bvh(const om_world& w, FrozenWorld& fw);
 }

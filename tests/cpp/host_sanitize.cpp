@@ -4,9 +4,13 @@
 // Built by `make -C tests/cpp sanitize` with -fsanitize=address,undefined (host code only, no
 // device code: the library's GPU kernels are not part of this binary), run by
 // tests/test_host_sanitize.py.  Any report aborts with a non-zero status.
+#include <cfloat>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <vector>
+
+#include "../../raytracingoneweekend_amd/csrc/om_bvh.h"
 
 #include "../../raytracingoneweekend_amd/csrc/om_shard.h"
 #include "../../raytracingoneweekend_amd/csrc/om_tiles.h"
@@ -42,7 +46,45 @@ static int g_fail = 0;
 
 struct Cam { float from[3], at[3], vup[3], vfov, aperture, focus; };
 
+// The half-precision BVH2 planes (OmBvh2NodeH, om_bvh.cpp) must round every f32 plane OUTWARD, or
+// an L2-resident tree could cull a box the exact test would hit: for every x,
+// value(half_out(x, lo)) <= x <= value(half_out(x, hi)), tight (neighbouring halves, or x itself
+// when x is a half), NaN -> the infinite planes, beyond +-65504 -> +-inf on the outer side.
+static int half_key(uint16_t h) { return (h & 0x8000u) ? -(int)(h & 0x7FFFu) : (int)h; }
+static void check_half_plane(float x) {
+    const uint16_t hl = om::half_out(x, false), hh = om::half_out(x, true);
+    const float lo = om::half_value(hl), hi = om::half_value(hh);
+    if (std::isnan(x)) { EXPECT(lo == -INFINITY && hi == INFINITY); return; }
+    EXPECT(lo <= x && x <= hi);
+    if (lo == x) { EXPECT(hi == x); return; }
+    EXPECT(half_key(hh) == half_key(hl) + 1 || (half_key(hl) == 0 && half_key(hh) == 1));
+}
+static void half_plane_sweep() {
+    std::vector<float> xs = {0.0f, -0.0f, INFINITY, -INFINITY, NAN, -NAN, FLT_MAX, -FLT_MAX, FLT_MIN, -FLT_MIN,
+                             1e-45f, -1e-45f, 65504.0f, -65504.0f, 65519.0f, 65520.0f, -65520.0f, 1e30f, -1e30f,
+                             5.96e-8f, 2.98e-8f, -2.98e-8f, 6.1e-5f, 1.0f, -1.0f, 1000.5f, -999.999f};
+    for (uint32_t h = 0; h < 0x10000u; ++h) {               // every half, and its f32 neighbours
+        const float v = om::half_value((uint16_t)h);
+        if (std::isinf(v)) continue;
+        xs.push_back(v); xs.push_back(std::nextafter(v, INFINITY)); xs.push_back(std::nextafter(v, -INFINITY));
+    }
+    uint64_t z = 0x9E3779B97F4A7C15ull;                       // random f32 bit patterns
+    for (int i = 0; i < 400000; ++i) {
+        z = z * 6364136223846793005ull + 1442695040888963407ull;
+        const uint32_t b = (uint32_t)(z >> 32);
+        float x;
+        std::memcpy(&x, &b, 4);
+        xs.push_back(x);
+        xs.push_back(std::ldexp((float)(b & 0xFFFFFF) / 16777216.0f - 0.5f, (int)(b >> 27) - 10));   // |x| ~ 2^-11..2^21
+    }
+    for (float x : xs) check_half_plane(x);
+    // an empty box (lo = +inf, hi = -inf) stays empty
+    EXPECT(om::half_value(om::half_out(INFINITY, false)) == INFINITY && om::half_value(om::half_out(-INFINITY, true)) == -INFINITY);
+    std::printf("half planes: %zu values round outward\n", xs.size());
+}
+
 int main() {
+    half_plane_sweep();
     const Cam cams[] = {
         {{13.f, 2.f, 3.f}, {0.f, 0.f, 0.f}, {0.f, 1.f, 0.f}, 20.f, 0.1f, 10.f},          // main.rs:136-142
         {{0.3f, 0.35f, 0.2f}, {5.f, 0.2f, 2.f}, {0.f, 1.f, 0.f}, 70.f, 1.5f, 2.f},         // wide lens inside the field
