@@ -51,6 +51,10 @@
 #ifndef OM_WF_TAIL_UNROLL
 #define OM_WF_TAIL_UNROLL 24
 #endif
+// marched tail: waves per SIMD requested (8: 64 VGPRs, the 24-step loop spills 32 B per lane)
+#ifndef OM_WF_TAIL_MARCH_WAVES
+#define OM_WF_TAIL_MARCH_WAVES 8
+#endif
 #ifndef OM_WF_TAIL_REFILL
 #define OM_WF_TAIL_REFILL OM_WF_REFILL
 #endif

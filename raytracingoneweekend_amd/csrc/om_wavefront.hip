@@ -673,7 +673,9 @@ __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const 
 }
 
 template <int TR, bool COUNT, bool MARCH, int VIEW = MV_ARRAYS, uint32_t SPB = kTailSpb>
-__global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_tail(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
+__global__ __launch_bounds__(kBlk) __attribute__((amdgpu_waves_per_eu(MARCH ? OM_WF_TAIL_MARCH_WAVES : OM_WF_WAVES,
+                                                                      MARCH ? OM_WF_TAIL_MARCH_WAVES : OM_WF_WAVES)))
+void k_tail(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
                                                const uint32_t* __restrict__ count_in, float4* __restrict__ res,
                                                uint32_t* __restrict__ res_id, unsigned long long* __restrict__ counters) {
     __shared__ uint32_t pre[SPB + 1];

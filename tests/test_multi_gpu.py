@@ -236,10 +236,13 @@ def test_multi_render_host_sees_a_rewritten_buffer(om, oracle):
     mf.close()
 
 
-def test_multi_adaptive_shards_bit_identical(om, oracle):
+@pytest.mark.parametrize("sched", [(0, 0), (5, 8)])
+def test_multi_adaptive_shards_bit_identical(om, oracle, sched):
     """Adaptive calls on shards: each logical rank renders its listed pixels
-    with concurrent 16-sample batches from per-stream snapshots of ITS shard; the gathered frame ==
-    one ctx rendering the whole frame adaptively, and a window of it == the sequential oracle."""
+    with the live-list schedule over ITS shard (its streams' chunks of the shard's list, the
+    batches planned from the live counts; `sched` = om_set_adaptive_batches on every rank, (5, 8):
+    several batches per stream); the gathered frame == one ctx rendering the whole frame
+    adaptively, and a window of it == the sequential oracle."""
     import torch
     from raytracingoneweekend_amd import _lib as L
     from raytracingoneweekend_amd import shard
@@ -253,6 +256,8 @@ def test_multi_adaptive_shards_bit_identical(om, oracle):
     torch.cuda.synchronize()
     fz.close()
     mf = shard.MultiFrame([0, 0, 0], world)
+    for r in range(3):
+        L.check(L.lib.om_set_adaptive_batches(mf.ctx(r), *sched), mf.ctx(r))
     s = torch.cuda.Stream()
     frame = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
     torch.cuda.synchronize()

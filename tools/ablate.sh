@@ -42,6 +42,8 @@ declare -A V=(
   # marched tail: ended lanes shaded together once this many wait
   [tm0]="$COMMON $DEV -DOM_WF_TAIL_MARCHED=0"
   [tm0l16]="$COMMON $DEV -DOM_WF_TAIL_MARCHED=0 -DOM_WF_LANES_PER_CU_WIDE=16384"
+  [tmw7]="$COMMON $DEV -DOM_WF_TAIL_MARCH_WAVES=7"
+  [tmw6]="$COMMON $DEV -DOM_WF_TAIL_MARCH_WAVES=6"
   [tsh1]="$COMMON $DEV -DOM_WF_TAIL_SHADE=1"
   [tsh4]="$COMMON $DEV -DOM_WF_TAIL_SHADE=4"
   [tsh8]="$COMMON $DEV -DOM_WF_TAIL_SHADE=8"
