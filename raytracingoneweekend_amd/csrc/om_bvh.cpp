@@ -7,6 +7,13 @@
 #include <cstring>
 #include <vector>
 
+#ifndef OM_BVH_MAX_LEAF
+#define OM_BVH_MAX_LEAF 8
+#endif
+#ifndef OM_BVH_TRAV
+#define OM_BVH_TRAV 1.0
+#endif
+
 namespace om {
 namespace {
 
@@ -118,11 +125,11 @@ struct Builder {
             }
         }
         const double leaf_cost = bb.area() * count;
-        // traversal cost relative to one primitive test; leaves <= 8 (a sweep of cost 0.3-2
-        // and max leaf 2-8 moved C1 by < 1%: the tree is not what bounds the kernel)
-        const double trav = 1.0 * bb.area();
+        // traversal cost relative to one primitive test (OM_BVH_TRAV); leaves <= OM_BVH_MAX_LEAF (r01:
+        // a sweep of cost 0.3-2 and max leaf 2-8 moved C1 by < 1%; r05 re-check in DESIGN.md §10)
+        const double trav = OM_BVH_TRAV * bb.area();
         if (best_axis < 0 || depth >= kSahDepth) {
-            if (count <= 4 || (best_axis < 0 && count <= 8)) return make_leaf();
+            if (count <= std::min(4u, (uint32_t)OM_BVH_MAX_LEAF) || (best_axis < 0 && count <= 8)) return make_leaf();
             // degenerate centroids: median split on the longest box axis
             int ax = 0;
             for (int k = 1; k < 3; ++k) if (bb.hi[k] - bb.lo[k] > bb.hi[ax] - bb.lo[ax]) ax = k;
@@ -134,7 +141,7 @@ struct Builder {
             nodes[node].left = (int32_t)l; nodes[node].right = (int32_t)r;
             return node;
         }
-        if (count <= 8 && leaf_cost <= best_cost + trav) return make_leaf();
+        if (count <= OM_BVH_MAX_LEAF && leaf_cost <= best_cost + trav) return make_leaf();
         const int ax = best_axis;
         const double lo = cb.lo[ax], hi = cb.hi[ax];
         auto mid_it = std::partition(items.begin() + begin, items.begin() + end, [&](const Item& it) {

@@ -72,6 +72,11 @@ declare -A V=(
   [acc1]="$COMMON $DEV -DOM_ACC_GROUP=1"
   [acc4]="$COMMON $DEV -DOM_ACC_GROUP=4"
   [acc16]="$COMMON $DEV -DOM_ACC_GROUP=16"
+  # BVH builder: max SAH leaf size, traversal cost (host side, om_bvh.cpp)
+  [bl2]="$COMMON $DEV -DOM_BVH_MAX_LEAF=2"
+  [bl4]="$COMMON $DEV -DOM_BVH_MAX_LEAF=4"
+  [bt05]="$COMMON $DEV -DOM_BVH_TRAV=0.5"
+  [bt2]="$COMMON $DEV -DOM_BVH_TRAV=2.0"
   # LLVM AMDGPU scheduler strategies (same code, different instruction order)
   [ilp]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-ilp"
   [memclause]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-memory-clause"
