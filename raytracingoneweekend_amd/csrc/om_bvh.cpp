@@ -7,8 +7,22 @@
 #include <cstring>
 #include <vector>
 
+// SAH leaves: at most OM_BVH_MAX_LEAF records, always a leaf at OM_BVH_LEAF_FORCE or fewer; a tree
+// whose compressed BVH2 does not fit the LDS budget (read through L2: S-10k) is rebuilt with the
+// _L2 sizes: one record per leaf, so a ray reads fewer 64-B records and more 32-B half nodes (r05:
+// C3 4258 / 4262 vs 4111 / 4119 Msamples/s at leaves <= 8, 4222 / 4240 at <= 2; C1, whose tree
+// sits in LDS, 6558 / 6561 at 1 and 6950 / 7016 at 2 vs 7003 / 7016: profiles/r05_bvh2)
 #ifndef OM_BVH_MAX_LEAF
 #define OM_BVH_MAX_LEAF 8
+#endif
+#ifndef OM_BVH_LEAF_FORCE
+#define OM_BVH_LEAF_FORCE 2
+#endif
+#ifndef OM_BVH_MAX_LEAF_L2
+#define OM_BVH_MAX_LEAF_L2 1
+#endif
+#ifndef OM_BVH_LEAF_FORCE_L2
+#define OM_BVH_LEAF_FORCE_L2 1
 #endif
 #ifndef OM_BVH_TRAV
 #define OM_BVH_TRAV 1.0
@@ -71,6 +85,7 @@ struct Builder {
     std::vector<Item> items;
     std::vector<OmBvhNode> nodes;
     std::vector<uint32_t> order;
+    uint32_t max_leaf = OM_BVH_MAX_LEAF, leaf_force = OM_BVH_LEAF_FORCE;
 
     uint32_t emit(const Box& b) {
         OmBvhNode n;
@@ -98,7 +113,7 @@ struct Builder {
             for (uint32_t i = begin; i < end; ++i) order.push_back(items[i].gi);
             return node;
         };
-        if (count <= 2) return make_leaf();
+        if (count <= leaf_force) return make_leaf();
         // binned SAH over the centroid box
         const int NB = 16;
         double best_cost = 1e300; int best_axis = -1; int best_bin = -1;
@@ -129,7 +144,7 @@ struct Builder {
         // a sweep of cost 0.3-2 and max leaf 2-8 moved C1 by < 1%; r05 re-check in DESIGN.md §10)
         const double trav = OM_BVH_TRAV * bb.area();
         if (best_axis < 0 || depth >= kSahDepth) {
-            if (count <= std::min(4u, (uint32_t)OM_BVH_MAX_LEAF) || (best_axis < 0 && count <= 8)) return make_leaf();
+            if (count <= std::min(4u, max_leaf) || (best_axis < 0 && count <= 8)) return make_leaf();
             // degenerate centroids: median split on the longest box axis
             int ax = 0;
             for (int k = 1; k < 3; ++k) if (bb.hi[k] - bb.lo[k] > bb.hi[ax] - bb.lo[ax]) ax = k;
@@ -141,7 +156,7 @@ struct Builder {
             nodes[node].left = (int32_t)l; nodes[node].right = (int32_t)r;
             return node;
         }
-        if (count <= OM_BVH_MAX_LEAF && leaf_cost <= best_cost + trav) return make_leaf();
+        if (count <= max_leaf && leaf_cost <= best_cost + trav) return make_leaf();
         const int ax = best_axis;
         const double lo = cb.lo[ax], hi = cb.hi[ax];
         auto mid_it = std::partition(items.begin() + begin, items.begin() + end, [&](const Item& it) {
@@ -256,7 +271,14 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     fw.snodes.clear();
     fw.srecs.clear();
     if (b.items.empty()) return;
-    const uint32_t root = b.build(0, (uint32_t)b.items.size());
+    uint32_t root = b.build(0, (uint32_t)b.items.size());
+    size_t internal = 0, leaves = 0;
+    for (const OmBvhNode& n : b.nodes) (n.left < 0 ? leaves : internal) += 1;
+    if (internal * sizeof(OmBvh2Node) + leaves * 4u > kB2LdsBudget) {    // read through L2: smaller leaves
+        b.nodes.clear(); b.order.clear();
+        b.max_leaf = OM_BVH_MAX_LEAF_L2; b.leaf_force = OM_BVH_LEAF_FORCE_L2;
+        root = b.build(0, (uint32_t)b.items.size());
+    }
     // depth-first re-emission with skip links
     std::vector<uint32_t> leaf_first(b.nodes.size(), 0);
     struct Emit {

@@ -152,6 +152,9 @@ struct OM_ALIGN16 OmBvh2NodeH {
     uint16_t c0, c1;
     uint32_t pad;
 };
+// f32 BVH2 nodes + leaf table of at most this many bytes are staged whole in LDS per workgroup;
+// a bigger tree is read through L2 (half nodes, an LDS prefix) and built with smaller leaves
+constexpr uint32_t kB2LdsBudget = 40u * 1024u;
 
 // Device view of a frozen world (passed by value as a kernel argument).
 struct OmSceneDev {

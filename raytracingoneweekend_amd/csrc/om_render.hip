@@ -645,7 +645,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     S.b2_direct = b2_ok ? fw.b2_direct : 0u;
     S.b2_stack = b2_ok ? fw.b2_depth : 0u;   // one push per internal level on the current path, deepest included
     const size_t b2_bytes = fw.b2nodes.size() * sizeof(OmBvh2Node) + fw.b2leaves.size() * 4u;
-    S.b2_lds_bytes = (b2_ok && b2_bytes <= 40u * 1024u) ? (uint32_t)((b2_bytes + 15u) & ~(size_t)15u) : 0u;
+    S.b2_lds_bytes = (b2_ok && b2_bytes <= kB2LdsBudget) ? (uint32_t)((b2_bytes + 15u) & ~(size_t)15u) : 0u;
     // BVH4 (same leaf table): up to 3 pushes per level + 3 spare entries for the
     // unconditional pushes, within the 48-entry bound of om_wavefront.hip
     const uint32_t b4_stack = 3u * fw.b4_depth + 3u;

@@ -75,6 +75,9 @@ declare -A V=(
   # BVH builder: max SAH leaf size, traversal cost (host side, om_bvh.cpp)
   [bl2]="$COMMON $DEV -DOM_BVH_MAX_LEAF=2"
   [bl4]="$COMMON $DEV -DOM_BVH_MAX_LEAF=4"
+  [bl1]="$COMMON $DEV -DOM_BVH_MAX_LEAF=1 -DOM_BVH_LEAF_FORCE=1"
+  [bl3]="$COMMON $DEV -DOM_BVH_MAX_LEAF=3"
+  [bl2t05]="$COMMON $DEV -DOM_BVH_MAX_LEAF=2 -DOM_BVH_TRAV=0.5"
   [bt05]="$COMMON $DEV -DOM_BVH_TRAV=0.5"
   [bt2]="$COMMON $DEV -DOM_BVH_TRAV=2.0"
   # LLVM AMDGPU scheduler strategies (same code, different instruction order)
