@@ -518,6 +518,7 @@ def run_adaptive(args, spp=512, per_call=128, reps=3):
     frames = {}
     out = {}
     ctrs = {}
+    launches = {}
     for label, streams in (("concurrent", args.streams), ("serial", 1)):
         fz = world.freeze(cam, kernel=args.kernel, pipeline=args.pipeline)
         L.check(L.lib.om_set_streams(fz.ctx, streams), fz.ctx)
@@ -546,6 +547,17 @@ def run_adaptive(args, spp=512, per_call=128, reps=3):
             torch.cuda.synchronize()
             times.append(time.perf_counter() - t0)
             assert torch.equal(st, ref), "adaptive frame differs between reps / builds"
+        # bounce-family launches of one frame (the library's own count, timing mode 2), for the
+        # PMC traffic per frame; the same frame again, bit for bit
+        kt = L.om_kernel_times()
+        st.zero_()
+        L.check(L.lib.om_set_timing(fz.ctx, 2), fz.ctx)
+        frame()
+        torch.cuda.synchronize()
+        L.check(L.lib.om_get_kernel_times(fz.ctx, C.byref(kt)), fz.ctx)
+        L.check(L.lib.om_set_timing(fz.ctx, 0), fz.ctx)
+        assert torch.equal(st, ref), "timing changed the adaptive frame"
+        launches[label] = int(kt.launches[L.KT_CLASSES.index("bounce_span")])
         fz.close()
         dt = sorted(times)[len(times) // 2]
         frames[label] = ref
@@ -566,12 +578,21 @@ def run_adaptive(args, spp=512, per_call=128, reps=3):
              + FLOP_CAMERA_RAY * ctr.samples)
     nbytes = BYTES_PER_LATER_SEGMENT * max(0, ctr.segments - ctr.samples) + BYTES_PER_SAMPLE * ctr.samples
     pmc = pmc_fields("C1_adaptive")
+    # HBM traffic per frame: the PMC mean per bounce-family launch (profiles/pmc_traffic_C1_adaptive.json,
+    # empty planned batches included) x the frame's launches
+    traffic, traffic_src = None, None
+    tf = PMC_TRAFFIC.replace(".json", "_C1_adaptive.json")
+    if os.path.exists(tf) and args.kernel == "auto":
+        pm = json.load(open(tf))
+        traffic, traffic_src = pm["hbm_bytes_per_launch"] * launches["concurrent"], pm["source"]
     achieved = flops / dt / 1e12
     roof = {"bound": "valu", "achieved": round(achieved, 3), "peak": PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_TFLOPS, 4), "frac_of_issue_peak": round(achieved / ISSUE_PEAK_TFLOPS, 4),
             "kernel": "k_bounce0+k_bounce+k_tail (fused trace+shade), adaptive live-list batches",
             "timing": "median frame wall time (host clock around the 4 calls)",
             "flop_per_frame": round(flops), "algorithmic_bytes_per_frame": round(nbytes),
+            "launches_per_frame": launches["concurrent"], "traffic_per_frame": round(traffic) if traffic else None,
+            "traffic_source": traffic_src, "traffic_over_algorithmic": round(traffic / nbytes, 3) if traffic else None,
             "hbm_achieved_gbs": round(nbytes / dt / 1e9, 2),
             "valu_lane_utilisation": pmc_top(pmc, "valu_lane_utilisation"),
             "wait_any_frac": pmc_top(pmc, "wait_any_frac"), "pmc": pmc}
