@@ -263,7 +263,7 @@ om_status om_set_streams(om_ctx* ctx, uint32_t streams);
 /* Wavefront adaptive calls (the GPU form of ThreadPixels, render_thread.rs:68-102): each stream
  * keeps a list of its live pixels, compacted by every batch's accumulate, and runs at most
  * `batches` batches per call (0 = default 3; more when a batch would exceed 2^26 paths).  A
- * batch renders b samples of every listed pixel: enough for 2^paths_log2 paths (0 = default 23),
+ * batch renders b samples of every listed pixel: enough for 2^paths_log2 paths (0 = default 22),
  * at least an even share of the call's remaining samples over the batches left, at most the
  * remainder; samples past a pixel's retirement inside a batch are dropped in sample order.  A
  * pure scheduling knob: results are bit-identical for every value. */

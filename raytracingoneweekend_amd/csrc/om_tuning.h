@@ -79,7 +79,7 @@
 #define OM_WF_ADAPTIVE_BATCHES 3
 #endif
 #ifndef OM_WF_ADAPTIVE_PATHS_LOG2
-#define OM_WF_ADAPTIVE_PATHS_LOG2 23
+#define OM_WF_ADAPTIVE_PATHS_LOG2 22
 #endif
 // the queue capacity an adaptive call may raise its forced even share to (more batches beyond it)
 #ifndef OM_WF_ADAPTIVE_CAP_LOG2
