@@ -17,6 +17,7 @@
  *   om_world_add_plane    InfinitePlane::new                        traced.rs:86-88
  *   om_world_add_marched_sphere / _box   struct literals            marched.rs:50-54, 79-83
  *   om_world_add_marched_torus  MarchedTorus::new                   marched.rs:116-130
+ *   om_world_add_marched_sdf    HittableList += Arc<dyn Marched>    hits.rs:96-100, marched.rs:7-41
  *   om_world_random_scene / om_world_basic_scene  front-end builders  main.rs:37-110
  *   om_material_*         Material::new_*                           materials.rs:27-38
  *   om_camera_new         Camera::new                               camera.rs:38-59
@@ -165,6 +166,36 @@ om_status om_world_add_plane(om_world* w, const float center[3], const float nor
 om_status om_world_add_marched_sphere(om_world* w, const float center[3], float radius, const om_material* m);
 om_status om_world_add_marched_box(om_world* w, const float center[3], const float sizes[3], const om_material* m);
 om_status om_world_add_marched_torus(om_world* w, const float local_to_world[16], const float sizes[3], const om_material* m);
+/* A user marched object: the GPU form of `HittableList += Arc<dyn Marched>` (hits.rs:96-100), which
+ * the reference's march loop visits after the typed marched objects (hits.rs:312-319, 350-356).
+ * A Rust `impl Marched` cannot run on the device, so its local_sdf is given as a postfix program
+ * over a float stack (at most OM_SDF_MAX_OPS ops, stack depth <= OM_SDF_MAX_STACK, exactly one
+ * value left), evaluated at the local point p:
+ *   OM_SDF_SPHERE    a = cx cy cz r          push |p - c| - r
+ *   OM_SDF_BOX       a = cx cy cz sx sy sz   q = |p - c| - s: push |max(q, 0)| + min(max(q.x, q.y, q.z), 0)
+ *   OM_SDF_TORUS     a = cx cy cz R r        q = p - c: push |(|(q.x, q.z, 0)| - R, q.y, 0)| - r
+ *   OM_SDF_UNION / _INTERSECT / _SUBTRACT    b = pop, a = pop: push min(a, b) / max(a, b) / max(a, -b)
+ *   OM_SDF_ROUND     a = r                   top - r
+ * (the formulas and op order of marched.rs:56-58, 86-89, 133-138; |v| = Vec3::length).  The object's
+ * transform is MarchedTorus's (marched.rs:116-130, 139-151): local_to_world decomposed into TR and S,
+ * to_local(p) = W2L_TR . (p * w2l_s), sdf = local_sdf * min(l2w_s.xyz), and the normal is the
+ * trait's default get_outward_normal (central differences, marched.rs:19-44).  A program
+ * [OM_SDF_TORUS 0 0 0 R r] is bit for bit a MarchedTorus with sizes (R, r).  Invalid programs
+ * (unknown op, stack underflow or overflow, not one value left, non-finite parameters) are
+ * OM_ERR_INVALID. */
+enum { OM_SDF_SPHERE = 1, OM_SDF_BOX = 2, OM_SDF_TORUS = 3, OM_SDF_UNION = 4, OM_SDF_INTERSECT = 5,
+       OM_SDF_SUBTRACT = 6, OM_SDF_ROUND = 7 };
+#define OM_SDF_MAX_OPS 64
+#define OM_SDF_MAX_STACK 8
+typedef struct om_sdf_op {
+    int32_t op;       /* OM_SDF_* */
+    float a[7];       /* parameters (unused ones ignored) */
+} om_sdf_op;
+om_status om_world_add_marched_sdf(om_world* w, const float local_to_world[16], const om_sdf_op* ops, uint32_t n_ops,
+                                   const om_material* m);
+/* number of user marched objects (they follow the eight types of om_world_counts in the
+ * global index order, so their obj ids come last) */
+om_status om_world_marched_sdf_count(const om_world* w, uint32_t* n);
 /* counts[8] in type order: spheres, cubes, triangles, infinite_planes, parallelograms,
  * marched_spheres, marched_boxes, marched_torus (hits.rs:370-371) */
 om_status om_world_counts(const om_world* w, uint32_t counts[8]);

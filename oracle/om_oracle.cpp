@@ -449,6 +449,41 @@ static MTorus mtorus_new(const M4& l2w, V3 sizes, const Material& m) {          
     return o;
 }
 
+// A user marched object (`HittableList += Arc<dyn Marched>`, hits.rs:96-100), the form the product
+// accepts (om_world_add_marched_sdf, include/ottomarcher.h): MarchedTorus's transform and default
+// trait methods (marched.rs:14-44, 139-151) around a local_sdf given as a postfix program.
+struct MSdfOp { int32_t op; float a[7]; };
+struct MSdf { MTorus xf; std::vector<MSdfOp> ops; Material mat; uint64_t id; };
+enum { SDF_SPHERE = 1, SDF_BOX = 2, SDF_TORUS = 3, SDF_UNION = 4, SDF_INTERSECT = 5, SDF_SUBTRACT = 6, SDF_ROUND = 7 };
+static float msdf_local_sdf(const MSdf& q, V3 p) {
+    float st[8]; int sp = 0;
+    for (const MSdfOp& o : q.ops) {
+        V3 c = v3(o.a[0], o.a[1], o.a[2]);
+        float v;
+        if (o.op == SDF_SPHERE) v = length(p - c) - o.a[3];                                  // as marched.rs:57-59
+        else if (o.op == SDF_BOX) {                                                          // as marched.rs:86-89
+            V3 b = vabs(p - c) - v3(o.a[3], o.a[4], o.a[5]);
+            v = length(vmax(b, v3(0, 0, 0))) + std::fmin(std::fmax(b.x, std::fmax(b.y, b.z)), 0.0f);
+        } else if (o.op == SDF_TORUS) {                                                      // as marched.rs:134-138
+            V3 pc = p - c;
+            V3 t = v3(length(v3(pc.x, pc.z, 0.0f)) - o.a[3], pc.y, 0.0f);
+            v = length(t) - o.a[4];
+        } else if (o.op == SDF_ROUND) v = st[--sp] - o.a[0];
+        else {
+            float b = st[--sp], a = st[--sp];
+            v = o.op == SDF_UNION ? std::fmin(a, b) : o.op == SDF_INTERSECT ? std::fmax(a, b) : std::fmax(a, -b);
+        }
+        st[sp++] = v;
+    }
+    return st[0];
+}
+static inline float msdf_sdf(const MSdf& q, V3 p) { return mtorus_to_world_f(q.xf, msdf_local_sdf(q, xyz(mtorus_to_local(q.xf, v4_p3(p))))); }
+static V3 msdf_normal(const MSdf& q, V3 p) {                                                 // default get_outward_normal
+    V3 lp = xyz(mtorus_to_local(q.xf, v4_p3(p)));
+    V4 n = v4_v3(outward_local_normal([&](V3 x) { return msdf_local_sdf(q, x); }, lp));
+    return unit(xyz(mtorus_to_world(q.xf, n)));
+}
+
 // ----------------------------------------------------------------------------
 // hits.rs: HittableList / FrozenHittableList::hit / unstuck
 // ----------------------------------------------------------------------------
@@ -458,6 +493,7 @@ struct World {
     std::vector<Sphere> spheres; std::vector<Cube> cubes; std::vector<Bary> triangles;
     std::vector<Plane> planes; std::vector<Bary> parallelograms;
     std::vector<MSphere> msph; std::vector<MBox> mbox; std::vector<MTorus> mtor;
+    std::vector<MSdf> msdf;                                                                  // Arc<dyn Marched>, after the typed ones
     uint32_t march_steps = 1024;                                                             // hits.rs:292
     // obj_id = global type-order index + 1 (0 = sky); replaces the memory address of utils.rs:110.
     void assign_ids() {
@@ -470,14 +506,16 @@ struct World {
         for (auto& o : msph) o.id = k++;
         for (auto& o : mbox) o.id = k++;
         for (auto& o : mtor) o.id = k++;
+        for (auto& o : msdf) o.id = k++;
     }
-    bool has_marched() const { return !msph.empty() || !mbox.empty() || !mtor.empty(); }
+    bool has_marched() const { return !msph.empty() || !mbox.empty() || !mtor.empty() || !msdf.empty(); }
 };
 
-// 0 = sphere, 1 = box, 2 = torus
+// 0 = sphere, 1 = box, 2 = torus, 3 = user object
 static inline float marched_sdf_abs(const World& w, int kind, size_t i, V3 p) {
     if (kind == 0) return std::fabs(msphere_sdf(w.msph[i], p));
     if (kind == 1) return std::fabs(mbox_sdf(w.mbox[i], p));
+    if (kind == 3) return std::fabs(msdf_sdf(w.msdf[i], p));
     return std::fabs(mtorus_sdf(w.mtor[i], p));
 }
 
@@ -491,6 +529,7 @@ static float unstuck(const World& w, float t, const Ray& r) {                   
     for (size_t i = 0; i < w.msph.size(); ++i) { float nd = marched_sdf_abs(w, 0, i, p); if (nd < d) { d = nd; kind = 0; idx = i; } }
     for (size_t i = 0; i < w.mbox.size(); ++i) { float nd = marched_sdf_abs(w, 1, i, p); if (nd < d) { d = nd; kind = 1; idx = i; } }
     for (size_t i = 0; i < w.mtor.size(); ++i) { float nd = marched_sdf_abs(w, 2, i, p); if (nd < d) { d = nd; kind = 2; idx = i; } }
+    for (size_t i = 0; i < w.msdf.size(); ++i) { float nd = marched_sdf_abs(w, 3, i, p); if (nd < d) { d = nd; kind = 3; idx = i; } }   // hits.rs:350-356
     float aux = d;
     if (kind < 0) return INF_F;
     uint64_t guard = 0;
@@ -519,6 +558,7 @@ static bool world_hit(const World& w, const Ray& r, float tmin, float tmax, HitR
         for (size_t i = 0; i < w.msph.size(); ++i) { float d = marched_sdf_abs(w, 0, i, point); if (d < distance) { distance = d; kind = 0; idx = i; } }
         for (size_t i = 0; i < w.mbox.size(); ++i) { float d = marched_sdf_abs(w, 1, i, point); if (d < distance) { distance = d; kind = 1; idx = i; } }
         for (size_t i = 0; i < w.mtor.size(); ++i) { float d = marched_sdf_abs(w, 2, i, point); if (d < distance) { distance = d; kind = 2; idx = i; } }
+        for (size_t i = 0; i < w.msdf.size(); ++i) { float d = marched_sdf_abs(w, 3, i, point); if (d < distance) { distance = d; kind = 3; idx = i; } }   // hits.rs:312-319
         if (kind < 0) return have;                                                           // hits.rs:323
         if (distance < HIT_SIZE) {                                                           // hits.rs:325-327
             rec.t = t; rec.point = point;
@@ -526,7 +566,8 @@ static bool world_hit(const World& w, const Ray& r, float tmin, float tmax, HitR
             // function of (object, point): evaluating it once for the winner is identical.
             if (kind == 0) { rec.normal = msphere_normal(w.msph[idx], point); rec.material = w.msph[idx].mat; rec.obj_id = w.msph[idx].id; }
             else if (kind == 1) { rec.normal = mbox_normal(w.mbox[idx], point); rec.material = w.mbox[idx].mat; rec.obj_id = w.mbox[idx].id; }
-            else { rec.normal = mtorus_normal(w.mtor[idx], point); rec.material = w.mtor[idx].mat; rec.obj_id = w.mtor[idx].id; }
+            else if (kind == 2) { rec.normal = mtorus_normal(w.mtor[idx], point); rec.material = w.mtor[idx].mat; rec.obj_id = w.mtor[idx].id; }
+            else { rec.normal = msdf_normal(w.msdf[idx], point); rec.material = w.msdf[idx].mat; rec.obj_id = w.msdf[idx].id; }
             return true;
         }
         t += distance;                                                                       // hits.rs:330
@@ -886,6 +927,13 @@ void oro_world_add_marched_sphere(void* w, const float* c, float r, const OroMat
 void oro_world_add_marched_box(void* w, const float* c, const float* sz, const OroMaterial* m) {
     MBox b; b.center = ld3(c); b.sizes = ld3(sz); b.mat = to_mat(m); b.id = 0; ((World*)w)->mbox.push_back(b);
 }
+void oro_world_add_marched_sdf(void* w, const float* l2w, const void* ops, uint32_t n, const OroMaterial* m) {
+    MSdf q;
+    q.xf = mtorus_new(m4_load(l2w), v3(0, 0, 0), to_mat(m));
+    q.ops.assign((const MSdfOp*)ops, (const MSdfOp*)ops + n);
+    q.mat = to_mat(m); q.id = 0;
+    ((World*)w)->msdf.push_back(q);
+}
 void oro_world_add_marched_torus(void* w, const float* l2w, const float* sz, const OroMaterial* m) {
     ((World*)w)->mtor.push_back(mtorus_new(m4_load(l2w), ld3(sz), to_mat(m)));
 }
@@ -1040,9 +1088,15 @@ void oro_get_ray(const OroCamera* c, float u, float v, uint64_t state, float* ou
     st3(r.orig, out6); st3(r.dir, out6 + 3);
 }
 void oro_stats_add(void* st, const float* color, float depth, uint64_t id) { stats_add(*(PixelStats*)st, ld3(color), depth, id); }
-float oro_marched_sdf(void* wp, int kind, uint32_t i, const float* p) { return (kind == 0 ? msphere_sdf(((World*)wp)->msph[i], ld3(p)) : kind == 1 ? mbox_sdf(((World*)wp)->mbox[i], ld3(p)) : mtorus_sdf(((World*)wp)->mtor[i], ld3(p))); }
+float oro_marched_sdf(void* wp, int kind, uint32_t i, const float* p) {
+    World* w = (World*)wp;
+    return kind == 0 ? msphere_sdf(w->msph[i], ld3(p)) : kind == 1 ? mbox_sdf(w->mbox[i], ld3(p))
+         : kind == 3 ? msdf_sdf(w->msdf[i], ld3(p)) : mtorus_sdf(w->mtor[i], ld3(p));
+}
 void oro_marched_normal(void* wp, int kind, uint32_t i, const float* p, float* out) {
-    World* w = (World*)wp; V3 n = kind == 0 ? msphere_normal(w->msph[i], ld3(p)) : kind == 1 ? mbox_normal(w->mbox[i], ld3(p)) : mtorus_normal(w->mtor[i], ld3(p));
+    World* w = (World*)wp;
+    V3 n = kind == 0 ? msphere_normal(w->msph[i], ld3(p)) : kind == 1 ? mbox_normal(w->mbox[i], ld3(p))
+         : kind == 3 ? msdf_normal(w->msdf[i], ld3(p)) : mtorus_normal(w->mtor[i], ld3(p));
     st3(n, out);
 }
 

@@ -56,6 +56,7 @@ def _load():
         "oro_world_add_marched_sphere": (None, [vp, fp, C.c_float, mp]),
         "oro_world_add_marched_box": (None, [vp, fp, fp, mp]),
         "oro_world_add_marched_torus": (None, [vp, fp, fp, mp]),
+        "oro_world_add_marched_sdf": (None, [vp, fp, vp, C.c_uint32, mp]),
         "oro_world_counts": (None, [vp, C.POINTER(C.c_uint32)]),
         "oro_world_affine": (None, [vp, C.c_int, C.c_uint32, fp]),
         "oro_world_bary": (None, [vp, C.c_int, C.c_uint32, fp]),
@@ -106,6 +107,19 @@ def material(kind, albedo=(0., 0., 0.), fuzz=0., ior=0.):
     return m
 
 
+SDF_OP_DTYPE = np.dtype([("op", "<i4"), ("a", "<f4", 7)])   # om_sdf_op (include/ottomarcher.h)
+SDF_OPS = {"sphere": 1, "box": 2, "torus": 3, "union": 4, "intersect": 5, "subtract": 6, "round": 7}
+
+
+def sdf_ops(ops):
+    """[(name or code, param, ...), ...] -> om_sdf_op records."""
+    arr = np.zeros(len(ops), dtype=SDF_OP_DTYPE)
+    for i, o in enumerate(ops):
+        arr[i]["op"] = SDF_OPS.get(o[0], o[0]) if isinstance(o[0], str) else o[0]
+        arr[i]["a"][:len(o) - 1] = o[1:]
+    return arr
+
+
 class World:
     """HittableList restated on the CPU (hits.rs)."""
 
@@ -147,10 +161,18 @@ class World:
     def add_marched_torus(self, l2w, s, m):
         lib.oro_world_add_marched_torus(self.h, fp((C.c_float * 16)(*map(float, np.ravel(l2w)))), fp(f3(s)), C.byref(m))
 
+    def add_marched_sdf(self, l2w, ops, m):
+        """A user marched object (Arc<dyn Marched>): `ops` = [(op, params...), ...] as om_sdf_op."""
+        arr = sdf_ops(ops)
+        lib.oro_world_add_marched_sdf(self.h, fp((C.c_float * 16)(*map(float, np.ravel(l2w)))),
+                                      arr.ctypes.data_as(C.c_void_p), arr.size, C.byref(m))
+        self.n_sdf = getattr(self, "n_sdf", 0) + 1
+
     def counts(self):
+        """The eight typed counts (hits.rs:370-371), then the user marched objects."""
         out = (C.c_uint32 * 8)()
         lib.oro_world_counts(self.h, out)
-        return list(out)
+        return list(out) + [getattr(self, "n_sdf", 0)]
 
     def affine(self, kind, i):
         out = (C.c_float * 32)()

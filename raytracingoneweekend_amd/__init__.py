@@ -6,8 +6,8 @@ hand-written HIP kernels for gfx950.  This package is the Python mirror of the
 reference's Camera / Material / HittableList / render API over that C-ABI.
 """
 from . import _lib
-from .api import (Camera, Cube, FrozenHittableList, HittableList, InfinitePlane, MarchedBox, MarchedSphere,
-                  MarchedTorus, Mat4x4, Material, Parallelogram, PixelsBox, Sphere, Triangle, display, m4x4,
+from .api import (Camera, Cube, FrozenHittableList, HittableList, InfinitePlane, MarchedBox, MarchedSdf,
+                  MarchedSphere, MarchedTorus, Mat4x4, Material, Parallelogram, PixelsBox, Sphere, Triangle, display, m4x4,
                   make_params, render, write_bmp, write_ppm)
 from .scenes import basic_scene, default_camera, marched_scene, random_scene, random_scene_api
 

@@ -46,6 +46,20 @@ class om_counters(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("samples", "segments", "prim_tests", "pre_tests", "march_steps", "credited")]
 
 
+# om_sdf_op (include/ottomarcher.h): one op of a user marched object's SDF program
+SDF_OP_DTYPE = np.dtype([("op", "<i4"), ("a", "<f4", 7)])
+SDF_OPS = {"sphere": 1, "box": 2, "torus": 3, "union": 4, "intersect": 5, "subtract": 6, "round": 7}
+
+
+def sdf_ops(ops):
+    """[(name or OM_SDF_* code, param, ...), ...] -> a contiguous om_sdf_op array."""
+    arr = np.zeros(len(ops), dtype=SDF_OP_DTYPE)
+    for i, o in enumerate(ops):
+        arr[i]["op"] = SDF_OPS[o[0]] if isinstance(o[0], str) else int(o[0])
+        arr[i]["a"][:len(o) - 1] = o[1:]
+    return arr
+
+
 KT_CLASSES = ("bounce0", "bounce", "tail", "accumulate", "megakernel", "bounce_span")   # OM_KT_* order
 # draw_to_sdl modes (main.rs:360-367), OM_VIEW_* order
 VIEWS = ("normal", "samples", "sample_blur", "depth", "depth_blur", "ids", "id_blur")
@@ -68,7 +82,7 @@ EXPORTS = [
     "om_world_add_sphere", "om_world_add_sphere_radius", "om_world_add_cube", "om_world_add_cube_length",
     "om_world_add_triangle", "om_world_add_parallelogram", "om_world_add_triangle_basis",
     "om_world_add_parallelogram_basis", "om_world_add_plane", "om_world_add_marched_sphere",
-    "om_world_add_marched_box", "om_world_add_marched_torus", "om_world_counts", "om_world_export",
+    "om_world_add_marched_box", "om_world_add_marched_torus", "om_world_add_marched_sdf", "om_world_marched_sdf_count", "om_world_counts", "om_world_export",
     "om_world_random_scene", "om_world_basic_scene", "om_world_marched_scene", "om_create", "om_destroy",
     "om_last_error", "om_upload_world", "om_set_kernel", "om_render", "om_render_device",
     "om_render_device_pixels", "om_get_counters", "om_reset_counters", "om_set_counting", "om_set_pipeline",
@@ -139,6 +153,8 @@ def _load():
         "om_world_add_marched_sphere": (st, [vp, fp, C.c_float, mp]),
         "om_world_add_marched_box": (st, [vp, fp, fp, mp]),
         "om_world_add_marched_torus": (st, [vp, fp, fp, mp]),
+        "om_world_add_marched_sdf": (st, [vp, fp, vp, C.c_uint32, mp]),
+        "om_world_marched_sdf_count": (st, [vp, C.POINTER(C.c_uint32)]),
         "om_world_counts": (st, [vp, C.POINTER(C.c_uint32)]),
         "om_world_export": (st, [vp, C.c_int32, C.c_uint32, fp, C.c_uint32]),
         "om_world_random_scene": (st, [vp, C.c_uint64, C.c_uint32, C.c_int32]),

@@ -23,7 +23,7 @@ from ._lib import check, f3, fptr, lib
 
 __all__ = [
     "Material", "Mat4x4", "m4x4", "Camera", "Sphere", "Cube", "Triangle", "Parallelogram", "InfinitePlane",
-    "MarchedSphere", "MarchedBox", "MarchedTorus", "HittableList", "FrozenHittableList", "PixelsBox", "render",
+    "MarchedSphere", "MarchedBox", "MarchedTorus", "MarchedSdf", "HittableList", "FrozenHittableList", "PixelsBox", "render",
     "RenderStats",
 ]
 
@@ -243,6 +243,22 @@ class MarchedTorus(Sphere):
         return MarchedTorus(lambda w: lib.om_world_add_marched_torus(w, fptr(m.m), fptr(s), C.byref(mat.raw)))
 
 
+class MarchedSdf(Sphere):
+    """A user marched object, the device form of `HittableList += Arc<dyn Marched>` (hits.rs:96-100):
+    an `impl Marched` whose local_sdf is a postfix program of om_sdf_op (include/ottomarcher.h),
+    under MarchedTorus's transform and the trait's default normal (marched.rs:14-44, 139-151).
+
+        MarchedSdf.new(m4x4("TR", 0, 1, 0), [("box", 0, 0, 0, .5, .5, .5), ("sphere", 0, 0, 0, .65),
+                                             ("intersect",)], Material.new_metal((.8, .6, .2)))
+    """
+
+    @staticmethod
+    def new(m_local_to_world, ops, mat):
+        m, arr = m_local_to_world, L.sdf_ops(ops)
+        return MarchedSdf(lambda w: lib.om_world_add_marched_sdf(w, fptr(m.m), arr.ctypes.data_as(C.c_void_p), arr.size,
+                                                                C.byref(mat.raw)))
+
+
 # ---------------------------------------------------------------- hits.rs
 class HittableList:
     """hits.rs:37-110 — host-side list; `world += prim` appends in type order."""
@@ -266,8 +282,9 @@ class HittableList:
 
     def __iadd__(self, prim):
         if not isinstance(prim, _Prim):
-            # Arc<dyn Traced/Marched> user types (hits.rs:91-100) cannot cross the C-ABI
-            raise TypeError("only the reference's primitive types can be added to a device world")
+            # Arc<dyn Traced> user types (hits.rs:91-95) cannot cross the C-ABI; a user marched
+            # object is a MarchedSdf (an SDF program)
+            raise TypeError("only the reference's primitive types and MarchedSdf can be added to a device world")
         check(prim.add_to(self._w))
         return self
 
@@ -277,8 +294,10 @@ class HittableList:
     def counts(self):
         out = (C.c_uint32 * 8)()
         check(lib.om_world_counts(self._w, out))
+        n = C.c_uint32()
+        check(lib.om_world_marched_sdf_count(self._w, C.byref(n)))
         return dict(zip(["spheres", "cubes", "triangles", "infinite_planes", "parallelograms",
-                         "marched_spheres", "marched_boxes", "marched_torus"], list(out)))
+                         "marched_spheres", "marched_boxes", "marched_torus", "marched_sdf"], list(out) + [n.value]))
 
     def export(self, kind, index, n):
         out = (C.c_float * n)()

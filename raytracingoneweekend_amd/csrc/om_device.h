@@ -10,6 +10,7 @@
 #include <stdint.h>
 
 #include "om_layout.h"
+#include "../../include/ottomarcher.h"
 
 namespace omd {
 
@@ -256,6 +257,67 @@ __device__ __forceinline__ F3 mtorus_normal(const OmMTorus& T, F3 p) {
                     m[4] * n.x + m[5] * n.y + m[6] * n.z + m[7] * w0,
                     m[8] * n.x + m[9] * n.y + m[10] * n.z + m[11] * w0);
     return unit(f3(r.x * T.l2w_s[0], r.y * T.l2w_s[1], r.z * T.l2w_s[2]));
+}
+
+// A user marched object (`Arc<dyn Marched>`, hits.rs:96-100; om_world_add_marched_sdf): its
+// local_sdf is a postfix program over a float stack, evaluated in program order with the op
+// formulas of the typed objects (marched.rs:56-58, 86-89, 133-138).  The stack is eight named
+// registers selected by unrolled compares (a runtime-indexed array would live in scratch memory).
+struct SdfStack {
+    float v[OM_SDF_MAX_STACK];
+    __device__ __forceinline__ float get(uint32_t i) const {
+        float r = v[0];
+#pragma unroll
+        for (uint32_t k = 1; k < OM_SDF_MAX_STACK; ++k) r = i == k ? v[k] : r;
+        return r;
+    }
+    __device__ __forceinline__ void set(uint32_t i, float x) {
+#pragma unroll
+        for (uint32_t k = 0; k < OM_SDF_MAX_STACK; ++k) v[k] = i == k ? x : v[k];
+    }
+};
+__device__ __forceinline__ float msdf_local(const OmSdfOp* ops, uint32_t n, F3 p) {
+    SdfStack st;
+#pragma unroll
+    for (uint32_t k = 0; k < OM_SDF_MAX_STACK; ++k) st.v[k] = 0.0f;
+    uint32_t sp = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const OmSdfOp o = ops[i];
+        const F3 q = f3(p.x - o.a[0], p.y - o.a[1], p.z - o.a[2]);
+        float v;
+        if (o.op == OM_SDF_SPHERE) {
+            v = len3(q) - o.a[3];
+        } else if (o.op == OM_SDF_BOX) {
+            const F3 b = f3(fabsf(q.x) - o.a[3], fabsf(q.y) - o.a[4], fabsf(q.z) - o.a[5]);
+            v = len3(f3(fmaxf(b.x, 0.0f), fmaxf(b.y, 0.0f), fmaxf(b.z, 0.0f))) + fminf(fmaxf(b.x, fmaxf(b.y, b.z)), 0.0f);
+        } else if (o.op == OM_SDF_TORUS) {
+            const float qx = march_sqrt((q.x * q.x + q.z * q.z) + 0.0f * 0.0f) - o.a[3];
+            v = march_sqrt((qx * qx + q.y * q.y) + 0.0f * 0.0f) - o.a[4];
+        } else if (o.op == OM_SDF_ROUND) {
+            sp -= 1u;
+            v = st.get(sp) - o.a[0];
+        } else {                                          // UNION / INTERSECT / SUBTRACT: b = pop, a = pop
+            const float b = st.get(sp - 1u), a = st.get(sp - 2u);
+            sp -= 2u;
+            v = o.op == OM_SDF_UNION ? fminf(a, b) : o.op == OM_SDF_INTERSECT ? fmaxf(a, b) : fmaxf(a, -b);
+        }
+        st.set(sp, v);
+        sp += 1u;
+    }
+    return st.get(0);
+}
+__device__ __forceinline__ float msdf_sdf(const OmMSdf& Q, const OmSdfOp* ops, F3 p) {     // Marched::sdf marched.rs:14-18
+    return msdf_local(ops + Q.op_first, Q.op_count, mtorus_to_local(Q, p)) * Q.min_scale;
+}
+__device__ __forceinline__ F3 msdf_normal(const OmMSdf& Q, const OmSdfOp* ops, F3 p) {    // default get_outward_normal
+    const F3 lp = mtorus_to_local(Q, p);
+    const F3 n = outward_local_normal([&](F3 q) { return msdf_local(ops + Q.op_first, Q.op_count, q); }, lp);
+    const float* m = Q.l2w_tr;
+    const float w0 = 0.0f;
+    const F3 r = f3(m[0] * n.x + m[1] * n.y + m[2] * n.z + m[3] * w0,
+                    m[4] * n.x + m[5] * n.y + m[6] * n.z + m[7] * w0,
+                    m[8] * n.x + m[9] * n.y + m[10] * n.z + m[11] * w0);
+    return unit(f3(r.x * Q.l2w_s[0], r.y * Q.l2w_s[1], r.z * Q.l2w_s[2]));
 }
 
 // ---------------------------------------------------------------- materials.rs

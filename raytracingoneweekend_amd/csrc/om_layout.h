@@ -76,6 +76,22 @@ struct OM_ALIGN16 OmMTorus {
     float br;         // upper bound of (R + r) / min-w2l_s factor
     float pad_b[3];
 };
+// A user marched object (`HittableList += Arc<dyn Marched>`, hits.rs:96-100; om_world_add_marched_sdf):
+// MarchedTorus's transform fields (same names, so the torus's to_local / normal code serves both)
+// and its local_sdf as a postfix program ops[op_first .. op_first + op_count) (OmSdfOp).
+struct OM_ALIGN16 OmMSdf {
+    float l2w_tr[16];
+    float w2l_tr[16];
+    float l2w_s[4];
+    float w2l_s[4];
+    float min_scale;  // l2w_s.xyz().min_val(): to_world_f (marched.rs:148-150)
+    uint32_t op_first, op_count, pad;
+};
+struct OM_ALIGN16 OmSdfOp {
+    uint32_t op;      // OM_SDF_* (ottomarcher.h)
+    float a[7];
+};
+
 // Material (materials.rs:18-24), padded to 32 B.
 struct OM_ALIGN16 OmMaterial {
     float albedo[3];
@@ -162,16 +178,17 @@ struct OmSceneDev {
     const OmAffineTest* cube_test; const OmAffineHit* cube_hit; const OmBound* cube_bound;
     const OmBary* tri; const OmPlane* plane; const OmBary* para;
     const OmMSphere* msph; const OmMBox* mbox; const OmMTorus* mtor;
+    const OmMSdf* msdf; const OmSdfOp* msdf_ops;   // user marched objects (after the tori in gi order)
     const OmMaterial* mats;       // by global index gi
     const uint64_t* bloom;        // by obj_id (gi + 1); bloom[0] = 0
     const OmBvhNode* bvh;         // over bounded traced prims (spheres, cubes, tris, paras)
     const uint32_t* bvh_prims;    // leaf -> global index gi
-    uint32_t n_sph, n_cube, n_tri, n_plane, n_para, n_msph, n_mbox, n_mtor;
+    uint32_t n_sph, n_cube, n_tri, n_plane, n_para, n_msph, n_mbox, n_mtor, n_msdf;
     uint32_t n_bvh_nodes;
     uint32_t n_always;            // number of unbounded/huge prims tested outside the BVH
     const uint32_t* always;       // their global indices (ascending)
     // type offsets of the global index space
-    uint32_t off_cube, off_tri, off_plane, off_para, off_msph, off_mbox, off_mtor, n_total;
+    uint32_t off_cube, off_tri, off_plane, off_para, off_msph, off_mbox, off_mtor, off_msdf, n_total;
     // stackless BVH over the affine primitives (records carry gi | cube<<31 in `pad`)
     const OmSkipNode* snodes; const OmAffineTest* srecs; const uint32_t* always2;
     uint32_t n_snodes, n_srecs, n_always2;

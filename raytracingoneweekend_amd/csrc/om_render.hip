@@ -393,7 +393,7 @@ template <int MODE, int BLOCK>
 void go(bool count, uint64_t threads, uint32_t lds, hipStream_t stream, const OmSceneDev& S, const OmCamDev& C,
         const OmParamsDev& P, const float2* jt, om_pixel_stats* st, const uint32_t* px, unsigned long long* ctr) {
     const uint32_t blocks = (uint32_t)((threads + BLOCK - 1) / BLOCK);
-    const bool march = (S.n_msph + S.n_mbox + S.n_mtor) != 0u;
+    const bool march = (S.n_msph + S.n_mbox + S.n_mtor + S.n_msdf) != 0u;
     if (count && march)
         hipLaunchKernelGGL((render_kernel<MODE, BLOCK, true, true>), dim3(blocks), dim3(BLOCK), lds, stream, S, C, P, jt, st, px, ctr);
     else if (count)
@@ -620,7 +620,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     UP(sph_test, sph_test); UP(sph_hit, sph_hit); UP(sph_bound, sph_bound);
     UP(cube_test, cube_test); UP(cube_hit, cube_hit); UP(cube_bound, cube_bound);
     UP(tri, tri); UP(plane, plane); UP(para, para);
-    UP(msph, msph); UP(mbox, mbox); UP(mtor, mtor);
+    UP(msph, msph); UP(mbox, mbox); UP(mtor, mtor); UP(msdf, msdf); UP(msdf_ops, msdf_ops);
     UP(mats, mats); UP(bloom, bloom); UP(bvh, bvh); UP(bvh_prims, bvh_prims); UP(always, always);
     UP(snodes, snodes); UP(srecs, srecs); UP(always2, always2); UP(always2_rec, always2_rec); UP(b2nodes, b2nodes); UP(b2h, b2h); UP(b2leaves, b2leaves);
 #undef UP
@@ -628,9 +628,10 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     c->world_gen++;
     c->tiles_valid = false;
     S.n_sph = fw.counts[0]; S.n_cube = fw.counts[1]; S.n_tri = fw.counts[2]; S.n_plane = fw.counts[3]; S.n_para = fw.counts[4];
-    S.n_msph = fw.counts[5]; S.n_mbox = fw.counts[6]; S.n_mtor = fw.counts[7];
+    S.n_msph = fw.counts[5]; S.n_mbox = fw.counts[6]; S.n_mtor = fw.counts[7]; S.n_msdf = fw.counts[om::K_MSDF];
     S.off_cube = fw.offsets[1]; S.off_tri = fw.offsets[2]; S.off_plane = fw.offsets[3]; S.off_para = fw.offsets[4];
-    S.off_msph = fw.offsets[5]; S.off_mbox = fw.offsets[6]; S.off_mtor = fw.offsets[7]; S.n_total = fw.offsets[8];
+    S.off_msph = fw.offsets[5]; S.off_mbox = fw.offsets[6]; S.off_mtor = fw.offsets[7];
+    S.off_msdf = fw.offsets[om::K_MSDF]; S.n_total = fw.offsets[om::K_N];
     S.n_bvh_nodes = (uint32_t)fw.bvh.size();
     S.n_always = (uint32_t)fw.always.size();
     S.n_snodes = (uint32_t)fw.snodes.size(); S.n_srecs = (uint32_t)fw.srecs.size(); S.n_always2 = (uint32_t)fw.always2.size();

@@ -319,16 +319,20 @@ struct MarchedArrays {
     static constexpr uint32_t KS = 0u, KB = 0u, KT = 0u;      // 0: unbounded
     static constexpr bool INDEXED = true;
     static constexpr bool RELOAD = false;
+    static constexpr bool USER = true;                         // visits the user objects (OmMSdf) too
     const OmMSphere* s; const OmMBox* b; const OmMTorus* t;
-    uint32_t ns, nb, nt;
+    const OmMSdf* q; const OmSdfOp* qo;
+    uint32_t ns, nb, nt, nq;
     __device__ explicit MarchedArrays(const OmSceneDev& S)
-        : s(S.msph), b(S.mbox), t(S.mtor), ns(S.n_msph), nb(S.n_mbox), nt(S.n_mtor) {}
+        : s(S.msph), b(S.mbox), t(S.mtor), q(S.msdf), qo(S.msdf_ops), ns(S.n_msph), nb(S.n_mbox), nt(S.n_mtor),
+          nq(S.n_msdf) {}
 };
 template <uint32_t KS_, uint32_t KB_, uint32_t KT_>
 struct MarchedRegs {
     static constexpr uint32_t KS = KS_, KB = KB_, KT = KT_;
     static constexpr bool INDEXED = false;
     static constexpr bool RELOAD = false;
+    static constexpr bool USER = false;
     OmMSphere s[KS]; OmMBox b[KB]; OmMTorus t[KT];
     uint32_t ns, nb, nt;
     __device__ explicit MarchedRegs(const OmSceneDev& S) : ns(S.n_msph), nb(S.n_mbox), nt(S.n_mtor) {
@@ -339,7 +343,9 @@ struct MarchedRegs {
 #pragma unroll
         for (uint32_t i = 0; i < KT; ++i) if (i < nt) t[i] = S.mtor[i];
     }
-    __device__ static bool fits(const OmSceneDev& S) { return S.n_msph <= KS && S.n_mbox <= KB && S.n_mtor <= KT; }
+    __device__ static bool fits(const OmSceneDev& S) {
+        return S.n_msph <= KS && S.n_mbox <= KB && S.n_mtor <= KT && S.n_msdf == 0u;
+    }
 };
 using MarchedSmall = MarchedRegs<4, 2, 1>;   // S-marched (2, 1, 1), S-full (0, 0, 1)
 
@@ -368,6 +374,7 @@ struct MarchedExactLds {
     // re-read every step (a compiler-only fence in nearest_marched): hoisted out of the march loop
     // the parameters would sit in VGPRs (64 + 23 spilled) instead of LDS
     static constexpr bool RELOAD = true;
+    static constexpr bool USER = false;                        // (run_batch picks it only without user objects)
     static constexpr uint32_t ns = NS, nb = NB, nt = NT;
     struct Block { OmMSphere s[NS ? NS : 1]; OmMBox b[NB ? NB : 1]; MTorusSdf t[NT ? NT : 1]; };
     const OmMSphere* s; const OmMBox* b; const MTorusSdf* t;
@@ -424,6 +431,12 @@ __device__ __forceinline__ float nearest_marched(const M& m, F3 p, int& bk, uint
         const float v = fabsf(mtorus_sdf(T, p));
         if (v < best) { best = v; bk = 2; bi = i; }
     });
+    if constexpr (M::USER) {                                   // Arc<dyn Marched> objects last (hits.rs:312-319)
+        for (uint32_t i = 0; i < m.nq; ++i) {
+            const float v = fabsf(msdf_sdf(m.q[i], m.qo, p));
+            if (v < best) { best = v; bk = 3; bi = i; }
+        }
+    }
     return best;
 }
 
@@ -432,6 +445,7 @@ __device__ __forceinline__ float nearest_marched(const M& m, F3 p, int& bk, uint
 template <class M>
 __device__ __forceinline__ float sdf_one(const M& m, int kind, uint32_t idx, F3 q) {
     if constexpr (M::INDEXED) {
+        if constexpr (M::USER) if (kind == 3) return fabsf(msdf_sdf(m.q[idx], m.qo, q));
         return kind == 0 ? fabsf(msphere_sdf(m.s[idx], q)) : kind == 1 ? fabsf(mbox_sdf(m.b[idx], q)) : fabsf(mtorus_sdf(m.t[idx], q));
     } else {
         float v = 0.0f;
@@ -478,7 +492,7 @@ __device__ __forceinline__ int march_step(const OmSceneDev& S, const M& m, F3 o,
     const float best = nearest_marched(m, p, bk, bi);
     if (bk < 0) return 2;                                                      // hits.rs:323
     if (best < HIT) {                                                          // hits.rs:325-327
-        gi = (int)(bk == 0 ? S.off_msph + bi : bk == 1 ? S.off_mbox + bi : S.off_mtor + bi);
+        gi = (int)(bk == 0 ? S.off_msph + bi : bk == 1 ? S.off_mbox + bi : bk == 2 ? S.off_mtor + bi : S.off_msdf + bi);
         return 1;
     }
     t += best;                                                                 // hits.rs:330
@@ -511,7 +525,9 @@ __device__ __forceinline__ int march(const OmSceneDev& S, F3 o, F3 d, float tmin
 // test re-run with tmax = its root reproduces the same root bit for bit.
 // MARCH = false (worlds without marched primitives, a compile-time split like the trace's):
 // the marched winners' normal code (central differences, ~60 sqrt/div) is left out.
-template <bool MARCH = true>
+// USER: the world may hold user marched objects (OmMSdf): their normal runs the SDF program 7 times,
+// whose registers must not weigh on the kernels of worlds without them (C2's shade and tail).
+template <bool MARCH = true, bool USER = MARCH>
 __device__ __forceinline__ void finalize(const OmSceneDev& S, int gi, F3 o, F3 d, float tmin, float t, F3& point, F3& normal) {
     const uint32_t g = (uint32_t)gi;
     if (g < S.off_tri) {                                                       // Sphere / Cube
@@ -549,7 +565,8 @@ __device__ __forceinline__ void finalize(const OmSceneDev& S, int gi, F3 o, F3 d
     if (!MARCH) { normal = f3(0.0f, 0.0f, 0.0f); return; }                    // unreachable: no marched winner
     if (g < S.off_mbox) normal = msphere_normal(S.msph[g - S.off_msph], point);
     else if (g < S.off_mtor) normal = mbox_normal(S.mbox[g - S.off_mbox], point);
-    else normal = mtorus_normal(S.mtor[g - S.off_mtor], point);
+    else if (!USER || g < S.off_msdf) normal = mtorus_normal(S.mtor[g - S.off_mtor], point);
+    else normal = msdf_normal(S.msdf[g - S.off_msdf], S.msdf_ops, point);
 }
 
 }  // namespace omd

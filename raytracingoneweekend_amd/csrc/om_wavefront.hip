@@ -276,14 +276,14 @@ __device__ __forceinline__ int trace(const OmSceneDev& S, const OmParamsDev& P, 
 // handle_hit + ray_color's termination rules (render_thread.rs:105-143) for one
 // segment.  Returns true when the path continues (p advanced to the next segment);
 // otherwise the sample's (colour, depth, id) is written to its result slot.
-template <bool MARCH>
+template <bool MARCH, bool USER = MARCH>
 __device__ __forceinline__ bool shade_path(const OmSceneDev& S, const OmParamsDev& P, uint32_t depth_cap, Path& p,
                                            float closest, int best, float4* __restrict__ res,
                                            uint32_t* __restrict__ res_id) {
     float seg_depth; uint32_t seg_id;
     if (best >= 0) {                                                   // handle_hit, Some(hr)
         F3 point, normal;
-        finalize<MARCH>(S, best, p.o, p.d, P.tmin, closest, point, normal);
+        finalize<MARCH, USER>(S, best, p.o, p.d, P.tmin, closest, point, normal);
         F3 nd, att;
         scatter(S.mats[best], p.d, normal, p.g, nd, att);
         p.cur = mul(p.cur, att);
@@ -359,7 +359,7 @@ __device__ __forceinline__ bool gen_path(const OmParamsDev& P, const Gen& R, uin
 // LDS counter and appends its survivors with one LDS atomic, so the 8 waves never wait for each
 // other.  Queue order within a segment then depends on which wave finishes first; results are
 // keyed by slot and the RNG by (pixel, sample), never by queue position.
-template <int TR, bool COUNT, bool MARCH, bool FIRST, bool HIT = false>
+template <int TR, bool COUNT, bool MARCH, bool FIRST, bool HIT = false, bool USER = MARCH>
 __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmParamsDev P, Seg G, Gen R, Queue in,
                                                  const uint32_t* __restrict__ count_in, Queue out,
                                                  uint32_t* __restrict__ count_out, float4* __restrict__ res,
@@ -433,7 +433,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
                 } else {
                     best = trace<TR, MARCH>(S, P, T, p.o, p.d, closest, w);
                 }
-                keep = shade_path<MARCH>(S, P, depth_cap, p, closest, best, res, res_id);
+                keep = shade_path<MARCH, USER>(S, P, depth_cap, p, closest, best, res, res_id);
                 if (COUNT) segs++;
             }
         }
@@ -654,7 +654,7 @@ __device__ __forceinline__ uint32_t tail_march_lanes(const OmSceneDev& S, const 
         if (ended && (OM_WF_TAIL_SHADE <= 1 || __popcll(em) >= OM_WF_TAIL_SHADE || am == 0)) {
             if (COUNT) segs++;
             unpark();
-            if (shade_path<true>(S, P, depth_cap, p, closest, best, res, res_id)) begin();
+            if (shade_path<true, M::USER>(S, P, depth_cap, p, closest, best, res, res_id)) begin();
             else have = false;
         }
         const uint64_t want = __ballot(!have && !dry), busy = __ballot(have);
@@ -883,7 +883,7 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
     Timer& tm = *L.timer;
     const bool each = tm.mode == 1;
     uint32_t launches = 0;
-    const bool exact = MARCH && MarchedC2Lds::matches(L.S.n_msph, L.S.n_mbox, L.S.n_mtor);
+    const bool exact = MARCH && L.S.n_msdf == 0u && MarchedC2Lds::matches(L.S.n_msph, L.S.n_mbox, L.S.n_mtor);
     auto tail = [&](const Queue& in, const uint32_t* cin) {
         const int ti = each ? tm.begin(st) : -1;
         const uint32_t grid = (G.nseg + kTailSpb - 1u) / kTailSpb;
@@ -921,8 +921,12 @@ uint32_t run_batch(QueueSet& B, const Launch& L, hipStream_t st, Seg G, const Ge
                                    B.hit, L.counters);
             tm.end(ti, kc, st);
             ti = each ? tm.begin(st) : -1;
-            hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false, true>), dim3(G.nseg), dim3(kBlk), 0, st, L.S, L.P, G, R, in,
-                               cin, out, cout, B.res, B.res_id, L.counters, (const float2*)B.hit);
+            if (exact && exact_view_built<TR>())                       // no user objects (OmMSdf) in the world
+                hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false, true, false>), dim3(G.nseg), dim3(kBlk), 0, st, L.S, L.P, G,
+                                   R, in, cin, out, cout, B.res, B.res_id, L.counters, (const float2*)B.hit);
+            else
+                hipLaunchKernelGGL((k_bounce<TR, COUNT, MARCH, false, true>), dim3(G.nseg), dim3(kBlk), 0, st, L.S, L.P, G, R, in,
+                                   cin, out, cout, B.res, B.res_id, L.counters, (const float2*)B.hit);
             tm.end(ti, kc, st);
             launches += 2u;
         }
@@ -1040,7 +1044,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
         tr = L.S.n_b2nodes == 0 ? (L.S.n_bvh_nodes <= 1u ? TR_BRUTE : TR_BVH) : (L.S.b2_lds_bytes ? TR_BVH2_LDS : TR_BVH2_GLOBAL);
     // segments, a multiple of the tail grouping: 4096 lanes per CU (8 workgroups of 512) for
     // traced worlds whose BVH2 sits in LDS, 8192 for marched worlds and L2-resident trees
-    const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor) != 0u;
+    const bool march = (L.S.n_msph + L.S.n_mbox + L.S.n_mtor + L.S.n_msdf) != 0u;
     const uint32_t tail_at = L.tail_bounce ? L.tail_bounce
                            : march ? kTailMarched : tr == TR_BVH2_GLOBAL ? kTailL2
                            : adaptive ? OM_WF_ADAPTIVE_TAIL

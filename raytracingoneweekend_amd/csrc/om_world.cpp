@@ -169,10 +169,10 @@ void om_world::freeze(FrozenWorld& fw) const {
     fw = FrozenWorld();
     fw.counts[0] = (uint32_t)spheres.size(); fw.counts[1] = (uint32_t)cubes.size(); fw.counts[2] = (uint32_t)triangles.size();
     fw.counts[3] = (uint32_t)planes.size(); fw.counts[4] = (uint32_t)parallelograms.size(); fw.counts[5] = (uint32_t)msph.size();
-    fw.counts[6] = (uint32_t)mbox.size(); fw.counts[7] = (uint32_t)mtor.size();
+    fw.counts[6] = (uint32_t)mbox.size(); fw.counts[7] = (uint32_t)mtor.size(); fw.counts[8] = (uint32_t)msdf.size();
     fw.offsets[0] = 0;
-    for (int k = 0; k < 8; ++k) fw.offsets[k + 1] = fw.offsets[k] + fw.counts[k];
-    const uint32_t total = fw.offsets[8];
+    for (int k = 0; k < K_N; ++k) fw.offsets[k + 1] = fw.offsets[k] + fw.counts[k];
+    const uint32_t total = fw.offsets[K_N];
     fw.mats.resize(total);
     fw.bloom.resize((size_t)total + 1);
     fw.bloom[0] = 0;
@@ -246,6 +246,17 @@ void om_world::freeze(FrozenWorld& fw) const {
             o.pad_b[0] = o.pad_b[1] = o.pad_b[2] = 0.0f;
         }
         put_mat(fw.offsets[K_MTORUS] + (uint32_t)i, t.mat);
+    }
+    fw.msdf.resize(msdf.size());
+    fw.msdf_ops.clear();
+    for (size_t i = 0; i < msdf.size(); ++i) {
+        const MSdfPrim& q = msdf[i]; OmMSdf& o = fw.msdf[i];
+        q.xf.l2w_tr.store(o.l2w_tr); q.xf.w2l_tr.store(o.w2l_tr);
+        for (int k = 0; k < 4; ++k) { o.l2w_s[k] = q.xf.l2w_s.e[k]; o.w2l_s[k] = q.xf.w2l_s.e[k]; }
+        o.min_scale = std::fmin(q.xf.l2w_s.e[0], std::fmin(q.xf.l2w_s.e[1], q.xf.l2w_s.e[2]));   // as the torus
+        o.op_first = (uint32_t)fw.msdf_ops.size(); o.op_count = (uint32_t)q.ops.size(); o.pad = 0;
+        fw.msdf_ops.insert(fw.msdf_ops.end(), q.ops.begin(), q.ops.end());
+        put_mat(fw.offsets[K_MSDF] + (uint32_t)i, q.mat);
     }
     build_bvh(*this, fw);
 }
@@ -390,6 +401,45 @@ om_status om_world_add_marched_box(om_world* w, const float c[3], const float sz
 om_status om_world_add_marched_torus(om_world* w, const float l2w[16], const float sz[3], const om_material* m) {
     OM_CHECK_ADD(w && l2w && sz && valid_mat(m), "om_world_add_marched_torus");
     w->mtor.push_back(make_torus(Mat4::load(l2w), Vec3::load(sz), *m));
+    return OM_OK;
+}
+
+om_status om_world_add_marched_sdf(om_world* w, const float l2w[16], const om_sdf_op* ops, uint32_t n, const om_material* m) {
+    OM_CHECK_ADD(w && l2w && ops && valid_mat(m), "om_world_add_marched_sdf");
+    if (n == 0 || n > OM_SDF_MAX_OPS) return fail(OM_ERR_INVALID, "om_world_add_marched_sdf: 1..OM_SDF_MAX_OPS ops");
+    MSdfPrim p;
+    int depth = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        const om_sdf_op& q = ops[i];
+        int params = 0, pops = 0;
+        switch (q.op) {
+            case OM_SDF_SPHERE: params = 4; break;
+            case OM_SDF_BOX: params = 6; break;
+            case OM_SDF_TORUS: params = 5; break;
+            case OM_SDF_UNION: case OM_SDF_INTERSECT: case OM_SDF_SUBTRACT: pops = 2; break;
+            case OM_SDF_ROUND: params = 1; pops = 1; break;
+            default: return fail(OM_ERR_INVALID, "om_world_add_marched_sdf: unknown op");
+        }
+        for (int k = 0; k < params; ++k)
+            if (!std::isfinite(q.a[k])) return fail(OM_ERR_INVALID, "om_world_add_marched_sdf: non-finite parameter");
+        if (depth < pops) return fail(OM_ERR_INVALID, "om_world_add_marched_sdf: stack underflow");
+        depth += (pops == 2 ? -1 : pops == 1 ? 0 : 1);
+        if (depth > OM_SDF_MAX_STACK) return fail(OM_ERR_INVALID, "om_world_add_marched_sdf: stack deeper than OM_SDF_MAX_STACK");
+        OmSdfOp o;
+        o.op = (uint32_t)q.op;
+        for (int k = 0; k < 7; ++k) o.a[k] = k < params ? q.a[k] : 0.0f;
+        p.ops.push_back(o);
+    }
+    if (depth != 1) return fail(OM_ERR_INVALID, "om_world_add_marched_sdf: the program must leave exactly one value");
+    p.xf = make_torus(Mat4::load(l2w), Vec3::make(0.0f, 0.0f, 0.0f), *m);     // MarchedTorus::new's decomposition
+    p.mat = *m;
+    w->msdf.push_back(std::move(p));
+    return OM_OK;
+}
+
+om_status om_world_marched_sdf_count(const om_world* w, uint32_t* n) {
+    if (!w || !n) return fail(OM_ERR_INVALID, "om_world_marched_sdf_count: null pointer");
+    *n = (uint32_t)w->msdf.size();
     return OM_OK;
 }
 

@@ -18,8 +18,11 @@ struct PlanePrim { Vec3 center, normal; om_material mat; };          // Infinite
 struct MSpherePrim { Vec3 center; float radius; om_material mat; };  // marched.rs:50-54
 struct MBoxPrim { Vec3 center, sizes; om_material mat; };            // marched.rs:79-83
 struct MTorusPrim { Mat4 l2w_tr, w2l_tr; Vec4 l2w_s, w2l_s; Vec3 sizes; om_material mat; };  // marched.rs:105-113
+// a user marched object (Arc<dyn Marched>, hits.rs:96-100): MarchedTorus's transform + an SDF program
+struct MSdfPrim { MTorusPrim xf; std::vector<OmSdfOp> ops; om_material mat; };
 
-enum PrimKind { K_SPHERE = 0, K_CUBE = 1, K_TRI = 2, K_PLANE = 3, K_PARA = 4, K_MSPHERE = 5, K_MBOX = 6, K_MTORUS = 7 };
+enum PrimKind { K_SPHERE = 0, K_CUBE = 1, K_TRI = 2, K_PLANE = 3, K_PARA = 4, K_MSPHERE = 5, K_MBOX = 6, K_MTORUS = 7,
+                K_MSDF = 8, K_N = 9 };
 
 // Frozen image of a world: arrays laid out exactly as they are copied to HBM.
 struct FrozenWorld {
@@ -31,6 +34,8 @@ struct FrozenWorld {
     std::vector<OmMSphere> msph;
     std::vector<OmMBox> mbox;
     std::vector<OmMTorus> mtor;
+    std::vector<OmMSdf> msdf;          // user marched objects
+    std::vector<OmSdfOp> msdf_ops;     // their programs, back to back
     std::vector<OmMaterial> mats;      // by global index
     std::vector<uint64_t> bloom;       // by obj id
     std::vector<OmBvhNode> bvh;
@@ -48,8 +53,8 @@ struct FrozenWorld {
     uint32_t b2_direct = 0;            // 1: leaf child codes carry OM_LEAF | first_record << 4 | count (no table read)
     std::vector<OmBvh4Node> b4nodes;   // 4-wide tree collapsed from b2nodes (leaf codes index b2leaves)
     uint32_t b4_depth = 0;             // its depth
-    uint32_t counts[8];
-    uint32_t offsets[9];               // global index offset per kind, offsets[8] = total
+    uint32_t counts[K_N];
+    uint32_t offsets[K_N + 1];         // global index offset per kind, offsets[K_N] = total
 };
 
 uint64_t bloom_hash(uint64_t id);      // utils.rs:94-107
@@ -63,5 +68,6 @@ struct om_world {
     std::vector<om::MSpherePrim> msph;
     std::vector<om::MBoxPrim> mbox;
     std::vector<om::MTorusPrim> mtor;
+    std::vector<om::MSdfPrim> msdf;
     void freeze(om::FrozenWorld& fw) const;
 };

@@ -140,3 +140,46 @@ def nan_normal_world(om, O):
     w += om.MarchedBox((0., 0.5, 2.2), (3., 0.5, 0.4), lam[0]); ow.add_marched_box((0., 0.5, 2.2), (3., 0.5, 0.4), lam[1])
     w += om.MarchedSphere((4., 1., -1.5), 1., die[0]); ow.add_marched_sphere((4., 1., -1.5), 1., die[1])
     return w, ow
+
+
+def user_sdf_zoo(om, O, torus_as_program=False):
+    """User marched objects (`HittableList += Arc<dyn Marched>`, hits.rs:96-100) as SDF programs
+    (om_world_add_marched_sdf) beside typed marched objects: CSG with every op, non-uniform scales,
+    a rotated frame.  torus_as_program: the typed torus replaced by the program [torus 0 0 0 R r]
+    under the same transform, which must render the same bits (same object index, too)."""
+    w, ow = om.HittableList.new(), O.World()
+    lam = lambda c: (om.Material.new_lambertian(c), O.material("lambertian", c))
+    met = lambda c, f: (om.Material.new_metal_fuzz(c, f), O.material("metal", c, fuzz=f))
+    die = lambda i: (om.Material.new_dielectric(i), O.material("dielectric", ior=i))
+    m, om_ = lam((0.5, 0.5, 0.5))
+    w += om.MarchedSphere((0., -100., 0.), 100., m); ow.add_marched_sphere((0., -100., 0.), 100., om_)
+    m, om_ = met((0.7, 0.6, 0.5), 0.1)
+    w += om.MarchedBox((1.6, 0.35, -0.4), (0.3, 0.35, 0.2), m); ow.add_marched_box((1.6, 0.35, -0.4), (0.3, 0.35, 0.2), om_)
+    tor = om.m4x4("TR", -0.2, 0.7, 0.3) ^ om.m4x4("RX", 0.8) ^ om.m4x4("SC", 1.3, 0.8, 1.1)
+    m, om_ = die(1.4)
+    if torus_as_program:
+        ops = [("torus", 0., 0., 0., 0.45, 0.12)]
+        w += om.MarchedSdf.new(tor, ops, m); ow.add_marched_sdf(tor.to_numpy(), ops, om_)
+    else:
+        w += om.MarchedTorus.new(tor, (0.45, 0.12, 0.12), m); ow.add_marched_torus(tor.to_numpy(), (0.45, 0.12, 0.12), om_)
+    progs = [
+        # a rounded cube carved by a sphere, scaled non-uniformly
+        (om.m4x4("TR", -1.3, 0.55, -0.2) ^ om.m4x4("RY", 0.5) ^ om.m4x4("SC", 0.9, 1.2, 0.8),
+         [("box", 0., 0., 0., 0.35, 0.35, 0.35), ("round", 0.05), ("sphere", 0., 0.1, 0., 0.42), ("subtract",)],
+         met((0.9, 0.5, 0.3), 0.0)),
+        # a sphere intersected with a box, unioned with a torus ring around it
+        (om.m4x4("TR", 0.6, 0.45, 0.9) ^ om.m4x4("RZ", 0.3),
+         [("sphere", 0., 0., 0., 0.4), ("box", 0., 0., 0., 0.3, 0.3, 0.3), ("intersect",),
+          ("torus", 0., 0., 0., 0.45, 0.05), ("union",)],
+         lam((0.2, 0.7, 0.9))),
+        # three spheres in a row, unioned (deep stack)
+        (om.m4x4("TR", 0.2, 0.18, -1.2),
+         [("sphere", -0.4, 0., 0., 0.18), ("sphere", 0., 0., 0., 0.18), ("sphere", 0.4, 0., 0., 0.18),
+          ("union",), ("union",)],
+         die(1.5)),
+    ]
+    for l2w, ops, (m, om_) in progs:
+        w += om.MarchedSdf.new(l2w, ops, m); ow.add_marched_sdf(l2w.to_numpy(), ops, om_)
+    cam = om.Camera.new((2.6, 1.4, 3.2), (0., 0.4, -0.2), (0., 1., 0.), 40., 1.5, 0.02, 4.)
+    ocam = O.camera((2.6, 1.4, 3.2), (0., 0.4, -0.2), (0., 1., 0.), 40., 1.5, 0.02, 4.)
+    return w, ow, cam, ocam

@@ -111,3 +111,37 @@ def test_world_counts_type_order(om):
     assert sum(w.counts().values()) == 0
     with pytest.raises(TypeError):
         w += object()
+
+
+def test_marched_sdf_program_validation(om):
+    """om_world_add_marched_sdf (a user `impl Marched`, hits.rs:96-100) accepts well-formed postfix
+    programs and refuses malformed ones with OM_ERR_INVALID, on the host, before any device work."""
+    from raytracingoneweekend_amd import _lib
+    L = _lib.lib
+    w = om.HittableList.new()
+    mat = om.Material.new_lambertian((0.4, 0.4, 0.4))
+    eye = om.Mat4x4.identity()
+
+    def add(ops, n=None):
+        arr = _lib.sdf_ops(ops) if ops else np.zeros(1, dtype=_lib.SDF_OP_DTYPE)
+        return L.om_world_add_marched_sdf(w.handle, _lib.fptr(eye.m), arr.ctypes.data_as(C.c_void_p),
+                                          arr.size if n is None else n, C.byref(mat.raw))
+    ok = [[("sphere", 0, 0, 0, 1)],
+          [("box", 0, 0, 0, 1, 1, 1), ("round", 0.1)],
+          [("sphere", 0, 0, 0, 1), ("torus", 0, 0, 0, 1, 0.2), ("union",)],
+          [("sphere", 0, 0, 0, 1)] * 8 + [("union",)] * 7]
+    for ops in ok:
+        assert add(ops) == 0, L.om_last_error(None)
+    bad = [[("union",)],                                           # stack underflow
+           [("round", 0.1)],                                       # underflow
+           [("sphere", 0, 0, 0, 1), ("sphere", 0, 0, 0, 1)],       # two values left
+           [("sphere", 0, 0, 0, 1)] * 9 + [("union",)] * 8,        # deeper than OM_SDF_MAX_STACK
+           [(99, 0, 0, 0, 1)],                                     # unknown op
+           [("sphere", 0, 0, 0, float("nan"))],                    # non-finite parameter
+           [("sphere", 0, 0, 0, 1)] * 65]                          # more than OM_SDF_MAX_OPS
+    for ops in bad:
+        assert add(ops) == _lib.OM_ERR_INVALID, ops
+    assert add([("sphere", 0, 0, 0, 1)], n=0) == _lib.OM_ERR_INVALID
+    assert w.counts()["marched_sdf"] == len(ok)
+    w += om.MarchedSdf.new(eye, [("sphere", 0, 0, 0, 0.5)], mat)
+    assert w.counts()["marched_sdf"] == len(ok) + 1

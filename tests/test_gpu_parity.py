@@ -535,3 +535,44 @@ def test_live_progress_word(om, pipeline, adaptive):
         assert any(0 < v < seen[-1] for v in seen), "no progress seen inside the call"
     L.check(L.lib.om_reset_progress(fz.ctx), fz.ctx)
     assert prog[0] == 0
+
+
+@pytest.mark.parametrize("pipeline", PIPELINES)
+def test_user_sdf_zoo_bit_exact(om, oracle, pipeline):
+    """User marched objects (`HittableList += Arc<dyn Marched>`, hits.rs:96-100) as SDF programs
+    (om_world_add_marched_sdf): CSG with every op under non-uniform transforms, visited after the
+    typed marched objects in the march loop and unstuck (hits.rs:312-319, 350-356), their normals by
+    the trait's central differences (marched.rs:19-44) == the oracle, both pipelines."""
+    from scenes_common import user_sdf_zoo
+    w, ow, cam, ocam = user_sdf_zoo(om, oracle)
+    W, H, SPP = 72, 48, 5
+    got, exp, _ = _render_both(om, oracle, w, ow, cam, ocam, W, H, SPP, "auto", march_steps=512, pipeline=pipeline,
+                               seed=31)
+    nb, msg = compare_stats(got, exp, f"user sdf zoo/{pipeline}")
+    assert nb == 0, msg
+    for oid in (4, 5, 6):                                  # the three programs (after sphere, box, torus)
+        h = np.uint64(oracle.bloom_hash(oid))
+        assert int(((got["bloom"] & h) == h).sum()) > 0, f"user object {oid} not seen"
+
+
+def test_user_sdf_torus_program_equals_marched_torus(om, oracle):
+    """The program [torus 0 0 0 R r] is a MarchedTorus (marched.rs:133-151): on the GPU the two worlds
+    render identical frames (same object index, so bloom too), equal to the oracle; wavefront with
+    the concurrent batches and the adaptive live-list schedule (several batches per stream)."""
+    from raytracingoneweekend_amd import _lib as L
+    from scenes_common import user_sdf_zoo
+    W, H, SPP = 64, 40, 24
+    frames = []
+    for prog in (False, True):
+        w, ow, cam, ocam = user_sdf_zoo(om, oracle, torus_as_program=prog)
+        fz = w.freeze(cam, pipeline="wavefront")
+        L.check(L.lib.om_set_adaptive_batches(fz.ctx, 5, 8), fz.ctx)
+        pix = om.PixelsBox.new(W * H)
+        for c in (7, 17):
+            om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=33, adaptive=True, sample_count=c, march_steps=256)
+        frames.append(pix.pixels.copy())
+    assert np.array_equal(frames[0].view(np.uint8), frames[1].view(np.uint8))
+    exp, _ = oracle.render(ow, ocam, oracle.params(W, H, SPP, seed=33, adaptive=True, march_steps=256))
+    nb, msg = compare_stats(frames[1], exp, "torus program, adaptive")
+    assert nb == 0, msg
+    assert int(frames[1]["n"].min()) < SPP

@@ -154,6 +154,48 @@ def test_sdf_known_values(oracle):
     assert sdf(2, (1., 0., 0.)) == F(-0.25) and sdf(2, (0., 0., 0.)) == F(0.75)
 
 
+def test_user_sdf_program_known_values(oracle):
+    """A user marched object's SDF program (om_world_add_marched_sdf) under the identity transform:
+    each op against its closed form, including the CSG ops and a deep stack."""
+    w = oracle.World()
+    eye = np.eye(4, dtype=F)
+    progs = [[("sphere", 1., 0., 0., 0.5)],
+             [("box", 0., 0., 0., 1., 1., 1.)],
+             [("torus", 0., 0., 0., 1., 0.25)],
+             [("sphere", 0., 0., 0., 1.), ("sphere", 2., 0., 0., 1.), ("union",)],
+             [("sphere", 0., 0., 0., 1.), ("sphere", 2., 0., 0., 1.), ("intersect",)],
+             [("sphere", 0., 0., 0., 1.), ("sphere", 2., 0., 0., 1.), ("subtract",)],
+             [("box", 0., 0., 0., 1., 1., 1.), ("round", 0.25)],
+             [("sphere", 0., 0., 0., 1.), ("sphere", 1., 0., 0., 1.), ("sphere", 2., 0., 0., 1.), ("union",), ("union",)]]
+    for ops in progs:
+        w.add_marched_sdf(eye, ops, _lam(oracle))
+    sdf = lambda i, p: oracle.lib.oro_marched_sdf(w.h, 3, i, oracle.fp(oracle.f3(p)))
+    assert sdf(0, (3., 0., 0.)) == 1.5 and sdf(0, (1., 0., 0.)) == -0.5
+    assert sdf(1, (3., 0., 0.)) == 2.0 and sdf(1, (0., 0., 0.)) == -1.0
+    assert sdf(2, (1., 0., 0.)) == F(-0.25) and sdf(2, (0., 0., 0.)) == F(0.75)
+    assert sdf(3, (4., 0., 0.)) == 1.0 and sdf(3, (-2., 0., 0.)) == 1.0       # min(3, 1), min(1, 3)
+    assert sdf(4, (1., 0., 0.)) == 0.0 and sdf(4, (4., 0., 0.)) == 3.0        # max(0, 0), max(3, 1)
+    assert sdf(5, (-0.5, 0., 0.)) == -0.5 and sdf(5, (1.5, 0., 0.)) == 0.5    # max(-0.5, -1.5), max(0.5, 0.5)
+    assert sdf(6, (3., 0., 0.)) == 1.75
+    assert sdf(7, (5., 0., 0.)) == 2.0 and sdf(7, (-3., 0., 0.)) == 2.0
+
+
+def test_user_sdf_torus_program_renders_the_marched_torus(om, oracle):
+    """The program [torus 0 0 0 R r] under a MarchedTorus's transform IS that torus (same to_local,
+    local_sdf, to_world_f and default normal, marched.rs:14-44, 133-151; same object index): the
+    oracle renders the two worlds bit for bit alike, bloom included."""
+    from scenes_common import compare_stats, user_sdf_zoo
+    W, H, SPP = 24, 16, 2
+    _, ow_t, _, ocam = user_sdf_zoo(om, oracle, torus_as_program=False)
+    _, ow_p, _, _ = user_sdf_zoo(om, oracle, torus_as_program=True)
+    p = oracle.params(W, H, SPP, seed=9, march_steps=256)
+    a, _ = oracle.render(ow_t, ocam, p)
+    b, _ = oracle.render(ow_p, ocam, p)
+    nb, msg = compare_stats(b, a, "torus program vs MarchedTorus")
+    assert nb == 0, msg
+    assert int(np.count_nonzero(a["bloom"])) > 0
+
+
 def test_marched_normals(oracle):
     w = oracle.World()
     w.add_marched_box((0., 0., 0.), (1., 1., 1.), _lam(oracle))
