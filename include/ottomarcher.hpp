@@ -197,6 +197,17 @@ struct MarchedTorus {                                                           
     }
 };
 
+// A user marched object: the device form of `HittableList += Arc<dyn Marched>` (hits.rs:96-100), its
+// local_sdf a postfix program of om_sdf_op (ottomarcher.h) under MarchedTorus's transform.
+struct MarchedSdf {
+    Mat4x4 local_to_world;
+    std::vector<om_sdf_op> ops;
+    Material material;
+    static MarchedSdf new_(const Mat4x4& m_local_to_world, std::vector<om_sdf_op> ops, const Material& mat) {
+        return {m_local_to_world, std::move(ops), mat};
+    }
+};
+
 // ------------------------------------------------------------ hits.rs
 class FrozenHittableList;
 
@@ -250,6 +261,10 @@ public:
     }
     HittableList& operator+=(const MarchedTorus& t) {
         check(om_world_add_marched_torus(w_, t.local_to_world.e, t.local_sizes.data(), &t.material.raw));
+        return *this;
+    }
+    HittableList& operator+=(const MarchedSdf& q) {
+        check(om_world_add_marched_sdf(w_, q.local_to_world.e, q.ops.data(), (uint32_t)q.ops.size(), &q.material.raw));
         return *this;
     }
     void clear() { check(om_world_clear(w_)); }
