@@ -463,6 +463,23 @@ void build_bvh4(FrozenWorld& fw) {
         }
     } r{fw, kids, area};
     r.go(0, 1);
+    // breadth-first renumbering with half-precision planes (trees read through L2, §5.7)
+    fw.b4h.clear();
+    std::vector<uint32_t> order{0u}, pos(fw.b4nodes.size(), 0u);
+    for (size_t h = 0; h < order.size(); ++h)
+        for (uint16_t c : fw.b4nodes[order[h]].child)
+            if (c != OM_EMPTY && !(c & OM_LEAF)) { pos[c] = (uint32_t)order.size(); order.push_back(c); }
+    for (uint32_t n : order) {
+        const OmBvh4Node& N = fw.b4nodes[n];
+        OmBvh4NodeH o{};
+        for (int k = 0; k < 4; ++k) {
+            o.b[k] = half_out(N.lox[k], false); o.b[4 + k] = half_out(N.loy[k], false); o.b[8 + k] = half_out(N.loz[k], false);
+            o.b[12 + k] = half_out(N.hix[k], true); o.b[16 + k] = half_out(N.hiy[k], true); o.b[20 + k] = half_out(N.hiz[k], true);
+            const uint16_t c = N.child[k];
+            o.child[k] = (c == OM_EMPTY || (c & OM_LEAF)) ? c : (uint16_t)pos[c];
+        }
+        fw.b4h.push_back(o);
+    }
 }
 
 }  // namespace om

@@ -130,6 +130,15 @@ struct OM_ALIGN16 OmBvh4Node {
     uint32_t pad[2];
 };
 
+// The 4-wide node with half-precision child boxes (64 B, one cache line; trees read through L2):
+// planes rounded outward like OmBvh2NodeH, b = lox[4] loy[4] loz[4] hix[4] hiy[4] hiz[4].  Emitted
+// breadth-first, so an LDS prefix holds the top levels (om_wavefront.hip, OM_WF_HYB4_BYTES).
+struct OM_ALIGN16 OmBvh4NodeH {
+    uint16_t b[24];
+    uint16_t child[4];
+    uint32_t pad[2];
+};
+
 // Prim tested outside the BVH2 tree (always2), with a conservative box tested first:
 // inflated for triangles/parallelograms, infinite for planes and huge bounds.
 struct OM_ALIGN16 OmAlwaysRec {
@@ -204,6 +213,7 @@ struct OmSceneDev {
     uint32_t b2_direct;           // leaf codes are OM_LEAF | first_record << 4 | count (om_bvh.cpp), not table indices
     // BVH4 collapsed from the BVH2 (same leaf table / records / always2)
     const OmBvh4Node* b4nodes;
+    const OmBvh4NodeH* b4h;       // the same tree breadth-first with half-precision boxes (n_b4nodes nodes)
     uint32_t n_b4nodes;
     uint32_t b4_lds_bytes;        // node bytes when they fit the LDS budget, else 0 (global nodes)
     uint32_t b4_stack;            // lane-stack entries: 3 per level + 3 for the unconditional pushes

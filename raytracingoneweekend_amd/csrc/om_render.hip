@@ -652,6 +652,7 @@ om_status om_upload_world(om_ctx* c, const om_world* w) {
     const uint32_t b4_stack = 3u * fw.b4_depth + 3u;
     const bool b4_ok = b2_ok && !fw.b4nodes.empty() && fw.b4nodes.size() < 32768u && b4_stack <= 48u;
     if (b4_ok && (s = upload(c, fw.b4nodes, &S.b4nodes)) != OM_OK) return s;
+    if (b4_ok && (s = upload(c, fw.b4h, &S.b4h)) != OM_OK) return s;
     S.n_b4nodes = b4_ok ? (uint32_t)fw.b4nodes.size() : 0u;
     S.b4_stack = b4_ok ? b4_stack : 0u;
     const size_t b4_bytes = fw.b4nodes.size() * sizeof(OmBvh4Node) + fw.b2leaves.size() * 4u;

@@ -16,6 +16,11 @@ template <int K> __device__ __forceinline__ float b2p(const OmBvh2Node& N) {
 // A half-precision box plane (OmBvh2NodeH) as f32, exactly.
 __device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 template <int K> __device__ __forceinline__ float b2p(const OmBvh2NodeH& N) { return h2f(N.b[K]); }
+// Plane P (lox loy loz hix hiy hiz) of child k of a 4-wide node, f32 or half.
+template <int P> __device__ __forceinline__ float b4p(const OmBvh4Node& N, int k) {
+    return P == 0 ? N.lox[k] : P == 1 ? N.loy[k] : P == 2 ? N.loz[k] : P == 3 ? N.hix[k] : P == 4 ? N.hiy[k] : N.hiz[k];
+}
+template <int P> __device__ __forceinline__ float b4p(const OmBvh4NodeH& N, int k) { return h2f(N.b[P * 4 + k]); }
 
 // Slab-test min/max (kept as fminf/fmaxf: an inline-asm v_min/v_max variant that skips
 // LLVM's canonicalising v_max x,x of loop-carried operands measured 12% slower, because the
@@ -730,10 +735,12 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
 // hit children are ordered near-first by a 5-compare sorting network, the nearest is
 // visited next and the others go on the lane's LDS stack with three unconditional u16
 // writes (no divergent push branches; the stack holds 3 spare entries for them).
-template <int STRIDE, class Wk>
-__device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node* nodes, const uint32_t* leaves,
+// HYB (half nodes, trees read through L2): nodes [0, nl) are the breadth-first prefix in LDS.
+template <int STRIDE, class Wk, bool HYB = false, class Node = OmBvh4Node>
+__device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const Node* nodes, const uint32_t* leaves,
                                            const OmAffineTest* recs, uint16_t* stk,
-                                           F3 o, F3 d, float tmin, float& closest, Wk& w) {
+                                           F3 o, F3 d, float tmin, float& closest, Wk& w,
+                                           const Node* gnodes = nullptr, uint32_t nl = 0) {
     if (!isfinite(o.x + o.y + o.z + d.x + d.y + d.z)) return nonfinite_hit(S, closest);
     int best = -1;
     const float ix = inv_dir(d.x);
@@ -752,7 +759,7 @@ __device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node
             cur = stk[sp * STRIDE];
             continue;
         }
-        const OmBvh4Node& N = nodes[cur];
+        const Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
         w.add_pre(4);
         const float t_hi = closest * 1.0001f + 1e-3f;
         float key[4];
@@ -760,9 +767,9 @@ __device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const OmBvh4Node
         int n = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const float x0 = __builtin_fmaf(N.lox[k], ix, nox), x1 = __builtin_fmaf(N.hix[k], ix, nox);
-            const float y0 = __builtin_fmaf(N.loy[k], iy, noy), y1 = __builtin_fmaf(N.hiy[k], iy, noy);
-            const float z0 = __builtin_fmaf(N.loz[k], iz, noz), z1 = __builtin_fmaf(N.hiz[k], iz, noz);
+            const float x0 = __builtin_fmaf(b4p<0>(N, k), ix, nox), x1 = __builtin_fmaf(b4p<3>(N, k), ix, nox);
+            const float y0 = __builtin_fmaf(b4p<1>(N, k), iy, noy), y1 = __builtin_fmaf(b4p<4>(N, k), iy, noy);
+            const float z0 = __builtin_fmaf(b4p<2>(N, k), iz, noz), z1 = __builtin_fmaf(b4p<5>(N, k), iz, noz);
             const float tn = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
             const float tf = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
             const uint32_t c = N.child[k];

@@ -35,6 +35,22 @@
 #ifndef OM_WF_HYB_BYTES
 #define OM_WF_HYB_BYTES 16384
 #endif
+// The same for the half-precision 4-wide tree (OM_KERNEL_BVH4 on a tree too big for LDS, §5.7).
+// C3 (r05_b4h): 0 / 4 / 8 / 12 KB -> 4028 / 3943 / 3895-3918 / 3918 Msamples/s: lanes whose node
+// is in LDS and lanes whose node is not run both loads, so every node comes through L1/L2.
+#ifndef OM_WF_HYB4_BYTES
+#define OM_WF_HYB4_BYTES 0
+#endif
+// Survivor ordering (experiment): a later bounce on the LDS BVH2 first orders its
+// segment by a key of origin cell (8x8 over the tree's x-z extent) and direction octant, and its
+// waves then take the paths in key order (path records as 64-B AoS, so the reads stay whole
+// records).  0 = queue order.
+#ifndef OM_WF_SORT
+#define OM_WF_SORT 0
+#endif
+#ifndef OM_WF_QUEUE_AOS
+#define OM_WF_QUEUE_AOS OM_WF_SORT
+#endif
 // k_march refills its idle lanes once at least this many of a wave's 64 wait
 #ifndef OM_WF_REFILL
 #define OM_WF_REFILL 16

@@ -52,6 +52,7 @@ struct FrozenWorld {
     uint32_t b2_depth = 0;             // its depth (stack bound)
     uint32_t b2_direct = 0;            // 1: leaf child codes carry OM_LEAF | first_record << 4 | count (no table read)
     std::vector<OmBvh4Node> b4nodes;   // 4-wide tree collapsed from b2nodes (leaf codes index b2leaves)
+    std::vector<OmBvh4NodeH> b4h;      // the same tree breadth-first, half-precision boxes rounded outward
     uint32_t b4_depth = 0;             // its depth
     uint32_t counts[K_N];
     uint32_t offsets[K_N + 1];         // global index offset per kind, offsets[K_N] = total

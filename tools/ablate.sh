@@ -36,6 +36,13 @@ declare -A V=(
   [hyb8k]="$COMMON $DEV -DOM_WF_HYB_BYTES=8192"
   [hyb12k]="$COMMON $DEV -DOM_WF_HYB_BYTES=12288"
   [hyb20k]="$COMMON $DEV -DOM_WF_HYB_BYTES=20480"
+  # S-10k with --kernel bvh4: bytes of breadth-first half-precision BVH4 prefix in LDS (default 0)
+  [h4p8k]="$COMMON $DEV -DOM_WF_HYB4_BYTES=8192"
+  [h4p4k]="$COMMON $DEV -DOM_WF_HYB4_BYTES=4096"
+  [h4p12k]="$COMMON $DEV -DOM_WF_HYB4_BYTES=12288"
+  # later bounces in (origin cell, octant) key order within each segment; AoS path records alone
+  [sort]="$COMMON $DEV -DOM_WF_SORT=1"
+  [aos]="$COMMON $DEV -DOM_WF_QUEUE_AOS=1"
   # k_march: refill threshold, steps per refill check
   [refill8]="$COMMON $DEV -DOM_WF_REFILL=8"
   [refill24]="$COMMON $DEV -DOM_WF_REFILL=24"
