@@ -41,16 +41,6 @@
 #ifndef OM_WF_HYB4_BYTES
 #define OM_WF_HYB4_BYTES 0
 #endif
-// Survivor ordering (experiment): a later bounce on the LDS BVH2 first orders its
-// segment by a key of origin cell (8x8 over the tree's x-z extent) and direction octant, and its
-// waves then take the paths in key order (path records as 64-B AoS, so the reads stay whole
-// records).  0 = queue order.
-#ifndef OM_WF_SORT
-#define OM_WF_SORT 0
-#endif
-#ifndef OM_WF_QUEUE_AOS
-#define OM_WF_QUEUE_AOS OM_WF_SORT
-#endif
 // k_march refills its idle lanes once at least this many of a wave's 64 wait
 #ifndef OM_WF_REFILL
 #define OM_WF_REFILL 16

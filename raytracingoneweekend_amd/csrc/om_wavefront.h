@@ -19,7 +19,6 @@ struct QueueSet {
     uint32_t* res_id = nullptr;  // obj id (0xFFFFFFFF = no sample)
     uint32_t* counts = nullptr;  // per bounce, per queue segment: live rays
     float2* hit = nullptr;       // split march pipeline: (closest, winner) per queue slot
-    uint32_t* perm[2] = {nullptr, nullptr};  // OM_WF_SORT: per queue, a segment's positions in key order
     void release();
 };
 

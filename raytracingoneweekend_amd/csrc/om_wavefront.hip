@@ -35,10 +35,8 @@ namespace omw {
 
 void QueueSet::release() {
     for (int a = 0; a < 2; ++a) {
-        if (OM_WF_QUEUE_AOS) { q[a][1] = q[a][2] = nullptr; qr[a] = nullptr; }   // inside q[a][0]
         for (int b = 0; b < 3; ++b) { if (q[a][b]) (void)hipFree(q[a][b]); q[a][b] = nullptr; }
         if (qr[a]) (void)hipFree(qr[a]); qr[a] = nullptr;
-        if (perm[a]) (void)hipFree(perm[a]); perm[a] = nullptr;
     }
     if (res) (void)hipFree(res);
     if (res_id) (void)hipFree(res_id);
@@ -151,14 +149,11 @@ struct AdList {
     uint32_t j;              // batch index within the stream's call
 };
 
-// One path queue: o|depthf, d|first_id, throughput|segment, rng s|rng k|slot|-, as four SoA
-// arrays or (OM_WF_QUEUE_AOS) one 64-B record per path with the words interleaved (stride kQs).
+// One SoA path queue: o|depthf, d|first_id, throughput|segment, rng s|rng k|slot|-.
+// (SoA, not 64-B AoS records: AoS measured -22% on C1, r05_sort)
 struct Queue {
     float4* q0; float4* q1; float4* q2; uint4* qr;
-    uint32_t* perm;   // OM_WF_SORT
 };
-constexpr uint64_t kQs = OM_WF_QUEUE_AOS ? 4u : 1u;
-constexpr bool kSort = OM_WF_SORT != 0;
 
 // Primary-ray source of bounce 0 (render_thread.rs:176-192).
 struct Gen {
@@ -196,13 +191,13 @@ __device__ __forceinline__ V ld4(const V* q) {
     return v;
 }
 __device__ __forceinline__ void load_ray(const Queue& Q, uint64_t i, Path& p) {
-    const float4 a = ld4(Q.q0 + i * kQs), b = ld4(Q.q1 + i * kQs);
+    const float4 a = ld4(Q.q0 + i), b = ld4(Q.q1 + i);
     p.o = f3(a.x, a.y, a.z); p.depthf = a.w;
     p.d = f3(b.x, b.y, b.z); p.first_id = __float_as_uint(b.w);
 }
 __device__ __forceinline__ void load_rest(const Queue& Q, uint64_t i, Path& p) {
-    const float4 c = ld4(Q.q2 + i * kQs);
-    const uint4 r = ld4(Q.qr + i * kQs);
+    const float4 c = ld4(Q.q2 + i);
+    const uint4 r = ld4(Q.qr + i);
     p.cur = f3(c.x, c.y, c.z); p.seg = __float_as_uint(c.w);
     p.g.s = r.x; p.g.k = r.y; p.slot = r.z;
 }
@@ -212,10 +207,10 @@ __device__ __forceinline__ void st4(V* q, V v) {
     __builtin_nontemporal_store(v.z, &q->z); __builtin_nontemporal_store(v.w, &q->w);
 }
 __device__ __forceinline__ void store_path(const Queue& Q, uint64_t i, const Path& p) {
-    st4(Q.q0 + i * kQs, make_float4(p.o.x, p.o.y, p.o.z, p.depthf));
-    st4(Q.q1 + i * kQs, make_float4(p.d.x, p.d.y, p.d.z, __uint_as_float(p.first_id)));
-    st4(Q.q2 + i * kQs, make_float4(p.cur.x, p.cur.y, p.cur.z, __uint_as_float(p.seg)));
-    st4(Q.qr + i * kQs, make_uint4(p.g.s, p.g.k, p.slot, 0u));
+    st4(Q.q0 + i, make_float4(p.o.x, p.o.y, p.o.z, p.depthf));
+    st4(Q.q1 + i, make_float4(p.d.x, p.d.y, p.d.z, __uint_as_float(p.first_id)));
+    st4(Q.q2 + i, make_float4(p.cur.x, p.cur.y, p.cur.z, __uint_as_float(p.seg)));
+    st4(Q.qr + i, make_uint4(p.g.s, p.g.k, p.slot, 0u));
 }
 
 // Scene data a workgroup traces against: the BVH2/BVH4 nodes + leaf table staged in LDS behind
@@ -373,48 +368,6 @@ __device__ __forceinline__ bool gen_path(const OmParamsDev& P, const Gen& R, uin
     return true;
 }
 
-// OM_WF_SORT: writes in.perm[seg0 .. seg0+n) = the segment's positions ordered by key =
-// (Morton cell of the origin on an 8x8 grid over the tree's x-z extent) << 3 | direction octant,
-// a counting sort in LDS (every thread of the block calls it).
-constexpr uint32_t kSortBins = 512;
-__device__ __forceinline__ void order_segment(const Tracer& T, const Queue& in, uint64_t seg0, uint32_t n) {
-    __shared__ uint32_t hist[kSortBins];
-    for (uint32_t b = threadIdx.x; b < kSortBins; b += kBlk) hist[b] = 0u;
-    const OmBvh2Node& r = T.b2n[0];
-    const float lx = fminf(r.lo0[0], r.lo1[0]), hx = fmaxf(r.hi0[0], r.hi1[0]);
-    const float lz = fminf(r.lo0[2], r.lo1[2]), hz = fmaxf(r.hi0[2], r.hi1[2]);
-    const float sx = 8.0f / fmaxf(hx - lx, 1e-6f), sz = 8.0f / fmaxf(hz - lz, 1e-6f);
-    auto key = [&](uint32_t j) {
-        const float4 a = in.q0[(seg0 + j) * kQs], b = in.q1[(seg0 + j) * kQs];
-        const uint32_t cx = (uint32_t)fminf(fmaxf((a.x - lx) * sx, 0.0f), 7.0f);
-        const uint32_t cz = (uint32_t)fminf(fmaxf((a.z - lz) * sz, 0.0f), 7.0f);
-        uint32_t m = 0u;
-#pragma unroll
-        for (int k = 0; k < 3; ++k) m |= (((cx >> k) & 1u) << (2 * k)) | (((cz >> k) & 1u) << (2 * k + 1));
-        return (m << 3) | (b.x < 0.0f ? 1u : 0u) | (b.y < 0.0f ? 2u : 0u) | (b.z < 0.0f ? 4u : 0u);
-    };
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < n; j += kBlk) atomicAdd(&hist[key(j)], 1u);
-    __syncthreads();
-    if (threadIdx.x < 64u) {                          // exclusive scan: 8 bins per lane of wave 0
-        uint32_t v[kSortBins / 64], t = 0u;
-#pragma unroll
-        for (uint32_t k = 0; k < kSortBins / 64; ++k) { v[k] = hist[threadIdx.x * (kSortBins / 64) + k]; t += v[k]; }
-        uint32_t incl = t;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off, 64);
-            if ((int)threadIdx.x >= off) incl += y;
-        }
-        uint32_t base = incl - t;
-#pragma unroll
-        for (uint32_t k = 0; k < kSortBins / 64; ++k) { hist[threadIdx.x * (kSortBins / 64) + k] = base; base += v[k]; }
-    }
-    __syncthreads();
-    for (uint32_t j = threadIdx.x; j < n; j += kBlk) in.perm[seg0 + atomicAdd(&hist[key(j)], 1u)] = j;
-    __syncthreads();
-}
-
 // ---------------------------------------------------------------- bounce
 // Workgroup s: the paths of segment s of queue `in` (FIRST: the camera samples
 // [s*segcap, (s+1)*segcap) of the batch) -> survivors into segment s of `out`.
@@ -455,8 +408,6 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
     if (threadIdx.x == 0) { q_next = kBlk / 64u; q_out = 0u; }
     __syncthreads();
     const Tracer T = HIT ? Tracer{} : stage_scene<TR>(S);
-    constexpr bool SORT = kSort && !FIRST && !HIT && !MARCH && TR == TR_BVH2_LDS;
-    if constexpr (SORT) order_segment(T, in, seg0, n);
     const uint32_t depth_cap = P.max_depth > 1u ? P.max_depth : 1u;
     WorkT<COUNT> w;
     uint32_t segs = 0;
@@ -467,7 +418,7 @@ __global__ __launch_bounds__(kBlk) OM_WAVES_ATTR void k_bounce(OmSceneDev S, OmP
         Path p;
         uint32_t p_pixel = 0;
         if (jj < n) {
-            const uint64_t i = seg0 + (SORT ? in.perm[seg0 + jj] : jj);
+            const uint64_t i = seg0 + jj;
             bool live = true;
             if (FIRST) {
                 live = gen_path(P, R, stride, first0 + jj, p, p_pixel, res_id);
@@ -579,7 +530,7 @@ __device__ __forceinline__ void march_lanes(const OmSceneDev& S, const OmParamsD
     int best = -1;
     uint32_t iters = 0;
     auto start = [&]() {
-        const float4 a = in.q0[(seg0 + j) * kQs], b = in.q1[(seg0 + j) * kQs];
+        const float4 a = in.q0[seg0 + j], b = in.q1[seg0 + j];
         o = f3(a.x, a.y, a.z); d = f3(b.x, b.y, b.z);
         best = trace<TR, false>(S, P, T, o, d, closest, w);
         marching = march_begin(m, o, d, P.tmin, t);
@@ -919,14 +870,8 @@ hipError_t grow(Buffers& B, uint64_t cap, uint32_t counts_n, int nsets) {
         for (int k = 0; k < nsets; ++k) {
             QueueSet& S = B.set[k];
             for (int a = 0; a < 2; ++a) {
-                if (OM_WF_QUEUE_AOS) {
-                    if ((e = hipMalloc(&S.q[a][0], cap * 4u * sizeof(float4))) != hipSuccess) return e;
-                    S.q[a][1] = S.q[a][0] + 1; S.q[a][2] = S.q[a][0] + 2; S.qr[a] = (uint4*)(S.q[a][0] + 3);
-                } else {
-                    for (int b = 0; b < 3; ++b) if ((e = hipMalloc(&S.q[a][b], cap * sizeof(float4))) != hipSuccess) return e;
-                    if ((e = hipMalloc(&S.qr[a], cap * sizeof(uint4))) != hipSuccess) return e;
-                }
-                if (kSort && (e = hipMalloc(&S.perm[a], cap * sizeof(uint32_t))) != hipSuccess) return e;
+                for (int b = 0; b < 3; ++b) if ((e = hipMalloc(&S.q[a][b], cap * sizeof(float4))) != hipSuccess) return e;
+                if ((e = hipMalloc(&S.qr[a], cap * sizeof(uint4))) != hipSuccess) return e;
             }
             if ((e = hipMalloc(&S.res, cap * sizeof(float4))) != hipSuccess) return e;
             if ((e = hipMalloc(&S.res_id, cap * sizeof(uint32_t))) != hipSuccess) return e;
@@ -946,7 +891,7 @@ hipError_t grow(Buffers& B, uint64_t cap, uint32_t counts_n, int nsets) {
     return hipSuccess;
 }
 
-Queue queue(QueueSet& B, int k) { return Queue{B.q[k][0], B.q[k][1], B.q[k][2], B.qr[k], B.perm[k]}; }
+Queue queue(QueueSet& B, int k) { return Queue{B.q[k][0], B.q[k][1], B.q[k][2], B.qr[k]}; }
 
 // One batch: bounce 0 .. tail_at-1 as per-bounce launches, then the tail launch, all on `st`;
 // returns the number of bounce-family launches.

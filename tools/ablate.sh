@@ -40,9 +40,6 @@ declare -A V=(
   [h4p8k]="$COMMON $DEV -DOM_WF_HYB4_BYTES=8192"
   [h4p4k]="$COMMON $DEV -DOM_WF_HYB4_BYTES=4096"
   [h4p12k]="$COMMON $DEV -DOM_WF_HYB4_BYTES=12288"
-  # later bounces in (origin cell, octant) key order within each segment; AoS path records alone
-  [sort]="$COMMON $DEV -DOM_WF_SORT=1"
-  [aos]="$COMMON $DEV -DOM_WF_QUEUE_AOS=1"
   # k_march: refill threshold, steps per refill check
   [refill8]="$COMMON $DEV -DOM_WF_REFILL=8"
   [refill24]="$COMMON $DEV -DOM_WF_REFILL=24"

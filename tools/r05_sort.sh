@@ -1,6 +1,8 @@
 #!/bin/bash
 # GPU box: survivor ordering by (origin cell, octant) key (_abl/lib_sort.so) and AoS path records
 # alone (_abl/lib_aos.so) vs the default build: parity of both through OM_LIB, then C1/C4 A/B.
+# The two variants were built from commit 17acef0 (tools/ablate.sh sort / aos there); both lost
+# and the code was removed after it.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
