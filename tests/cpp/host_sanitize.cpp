@@ -83,6 +83,35 @@ static void half_plane_sweep() {
     std::printf("half planes: %zu values round outward\n", xs.size());
 }
 
+// The half-precision BVH4 (om_bvh.cpp build_bvh4): breadth-first (every internal child after its
+// parent, the root first), the same child codes as the f32 tree walked in step, and every half
+// box containing its f32 box (planes rounded outward), so the L2 tree culls conservatively.
+static void check_b4h(const om::FrozenWorld& fw) {
+    EXPECT(fw.b4h.size() == fw.b4nodes.size());
+    if (fw.b4nodes.empty()) return;
+    std::vector<std::pair<uint32_t, uint32_t>> q{{0u, 0u}};   // (f32 DFS node, half BFS node)
+    std::vector<uint32_t> seen(fw.b4h.size(), 0);
+    for (size_t h = 0; h < q.size(); ++h) {
+        const OmBvh4Node& F = fw.b4nodes[q[h].first];
+        const OmBvh4NodeH& N = fw.b4h[q[h].second];
+        seen[q[h].second]++;
+        for (int k = 0; k < 4; ++k) {
+            const uint16_t cf = F.child[k], ch = N.child[k];
+            EXPECT((cf == OM_EMPTY) == (ch == OM_EMPTY));
+            if (cf == OM_EMPTY) continue;
+            const float f[6] = {F.lox[k], F.loy[k], F.loz[k], F.hix[k], F.hiy[k], F.hiz[k]};
+            for (int a = 0; a < 3; ++a) {
+                EXPECT(om::half_value(N.b[a * 4 + k]) <= f[a]);
+                EXPECT(om::half_value(N.b[(3 + a) * 4 + k]) >= f[3 + a]);
+            }
+            if (cf & OM_LEAF) { EXPECT(ch == cf); continue; }
+            EXPECT(!(ch & OM_LEAF) && ch > q[h].second && ch < fw.b4h.size());
+            q.emplace_back(cf, ch);
+        }
+    }
+    for (uint32_t v : seen) EXPECT(v == 1u);
+}
+
 int main() {
     half_plane_sweep();
     const Cam cams[] = {
@@ -102,6 +131,7 @@ int main() {
         om::FrozenWorld fw;
         w->freeze(fw);                                          // BVH, SBVH, BVH2, BVH4 builders
         EXPECT(fw.offsets[8] > 0);
+        check_b4h(fw);
         size_t lists = 0;
         for (const Cam& c : cams)
             for (const auto& sz : sizes) {
