@@ -22,13 +22,15 @@ template <int P> __device__ __forceinline__ float b4p(const OmBvh4Node& N, int k
 }
 template <int P> __device__ __forceinline__ float b4p(const OmBvh4NodeH& N, int k) { return h2f(N.b[P * 4 + k]); }
 
-// Slab-test min/max (kept as fminf/fmaxf: an inline-asm v_min/v_max variant that skips
-// LLVM's canonicalising v_max x,x of loop-carried operands measured 12% slower, because the
-// compiler drains every outstanding load before an asm statement).
-__device__ __forceinline__ float smin(float a, float b) { return fminf(a, b); }
-__device__ __forceinline__ float smax(float a, float b) { return fmaxf(a, b); }
-__device__ __forceinline__ float smin3(float a, float b, float c) { return fminf(fminf(a, b), c); }
-__device__ __forceinline__ float smax3(float a, float b, float c) { return fmaxf(fmaxf(a, b), c); }
+// Slab-test min/max as IEEE minimum/maximum (NaN-propagating): gfx950's v_minimum3_f32 /
+// v_maximum3_f32 need no canonicalising v_max x,x of the loop-carried t_lo / t_hi that fminf /
+// fmaxf cost per node visit (an inline-asm v_min/v_max variant lost 12%: the compiler drains
+// every outstanding load before an asm statement).  Culling only: a NaN slab value
+// reaches near or far and every `!(near > far)` test then visits the box.
+__device__ __forceinline__ float smin(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+__device__ __forceinline__ float smax(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+__device__ __forceinline__ float smin3(float a, float b, float c) { return smin(smin(a, b), c); }
+__device__ __forceinline__ float smax3(float a, float b, float c) { return smax(smax(a, b), c); }
 // near / far slab distances of one box: max(min(x), min(y), min(z), t_lo), min(max(x), max(y), max(z), t_hi)
 __device__ __forceinline__ float slab_near(float x0, float x1, float y0, float y1, float z0, float z1, float t_lo) {
     return smax3(smin(x0, x1), smin(y0, y1), smax(smin(z0, z1), t_lo));
@@ -151,7 +153,7 @@ __device__ __forceinline__ int traced_bvh(const OmSceneDev& S, F3 o, F3 d, float
             z0 = (R.lo[2] - o.z) * iz; z1 = (R.hi[2] - o.z) * iz;
             const float rn = slab_near(x0, x1, y0, y1, z0, z1, t_lo);
             const float rf = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
-            const bool hl = ln <= lf, hr = rn <= rf;
+            const bool hl = !(ln > lf), hr = !(rn > rf);
             if (hl && hr) {
                 const bool left_first = ln <= rn;
                 stack[sp++] = left_first ? (uint32_t)N.right : (uint32_t)N.left;
@@ -716,7 +718,8 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
         bool h0, h1, swap;
         slabs(N, h0, h1, swap);
         if (h0 && h1) {                             // near child next, far child pushed
-            if (sp < DEPTH) { stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1); ++sp; }
+            stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1);   // sp < depth: om_upload_world sizes the stack
+            ++sp;
             cur = swap ? N.c1 : N.c0;
         } else if (h0 || h1) {
             cur = h0 ? N.c0 : N.c1;
