@@ -707,7 +707,7 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
     // leaf, then the wave's leaves are tested) -- written as one flat if/else loop instead,
     // C1 ran 14% slower (r04)
     for (;;) {
-        if (cur & OM_LEAF) {                        // the single leaf site
+        if (cur >= OM_LEAF) {                       // the single leaf site (16-bit codes: one compare, no and)
             test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
             if (sp == 0) break;
             --sp;
@@ -755,7 +755,7 @@ __device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const Node* node
     uint32_t cur = 0;
     int sp = 0;
     for (;;) {
-        if (cur & OM_LEAF) {
+        if (cur >= OM_LEAF) {
             test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
             if (sp == 0) break;
             --sp;
