@@ -106,9 +106,12 @@ enum {
     OM_KERNEL_CULLED = 2,      /* brute force + conservative bounding-sphere pre-test */
     OM_KERNEL_BVH = 3,         /* stack-based BVH traversal (global memory) with the brute-force tie rule */
     OM_KERNEL_SBVH = 4,        /* stackless skip-pointer BVH, staged in LDS when it fits */
-    OM_KERNEL_BVH2 = 5,        /* compressed BVH2, LDS nodes + LDS lane stack (AUTO, both pipelines) */
-    OM_KERNEL_BVH4 = 6         /* 4-wide BVH collapsed from the BVH2, sorted near-first, LDS nodes +
-                                  LDS lane stack (the megakernel runs OM_KERNEL_BVH2 for it) */
+    OM_KERNEL_BVH2 = 5,        /* compressed BVH2 + LDS lane stack (AUTO, both pipelines): f32 nodes in LDS,
+                                  or, for a tree over the LDS budget, half-precision nodes through L2
+                                  behind a breadth-first LDS prefix */
+    OM_KERNEL_BVH4 = 6         /* 4-wide BVH collapsed from the BVH2, sorted near-first, LDS lane stack:
+                                  f32 nodes in LDS, or half-precision nodes through L2 for a tree over the
+                                  LDS budget (the megakernel runs OM_KERNEL_BVH2 for it) */
 };
 
 /* Work counters of the last render call (device atomics, wave-aggregated). */
