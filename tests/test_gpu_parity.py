@@ -175,6 +175,24 @@ def test_ten_k_scene_bvh_bit_exact(om, oracle, kernel):
     assert nb == 0, msg
 
 
+def test_ten_k_half_bvh4_adaptive_and_tail_bit_exact(om, oracle):
+    """The half-precision 4-wide tree read through L2 (OM_KERNEL_BVH4 on S-10k): a
+    wider frame than test_ten_k_scene_bvh_bit_exact, adaptive sampling, and the persistent tail
+    from bounce 2, so most segments run in the tail's traversal."""
+    from raytracingoneweekend_amd import _lib as L
+    W, H, SPP = 48, 27, 6
+    world = om.random_scene(0x5EED, grid_half=50, extras=False)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam, kernel="bvh4", pipeline="wavefront")
+    L.check(L.lib.om_set_tail_bounce(fz.ctx, 2), fz.ctx)
+    pix = om.PixelsBox.new(W * H)
+    om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, pix, seed=9, adaptive=True)
+    p = oracle.params(W, H, SPP, adaptive=True, seed=9)
+    exp, _ = oracle.render(oracle.random_scene(0x5EED, grid_half=50, extras=False), oracle.default_camera(W / H), p)
+    nb, msg = compare_stats(pix.pixels, exp, "S-10k/bvh4-half")
+    assert nb == 0, msg
+
+
 @pytest.mark.parametrize("pipeline", PIPELINES)
 def test_counters_consistent(om, pipeline):
     W, H, SPP = 32, 16, 4
