@@ -205,11 +205,105 @@ class Control:
             dist.destroy_process_group()
 
 
-def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_mode, pmc_ok=True):
-    """One config through the product path; returns the measured fields (value, roofline, work)."""
+def layout(name, n, rank, spp_per_step, steps):
+    """The rank's share of a config's job: (W, H, depth, spp_step, spp_total, cap, n_mine).  Every
+    config but C4 is weak scaling (a rank renders its 1/n of the tiles at spp_per_step * n samples
+    per step: fixed per-GPU work); C4 renders the fixed 4K frame (strong scaling)."""
     cfg = CONFIGS[name]
     W, H = cfg.get("size", (1920, 1080))
     depth = cfg.get("depth", MAX_DEPTH)
+    spp_step = spp_per_step * (1 if name == "C4" else n)
+    cap = shard.shard_capacity(W, H, n)
+    n_mine = shard.tile_pixels(W, H, rank, n).size
+    return W, H, depth, spp_step, spp_step * steps, cap, n_mine
+
+
+def check_gathered(shard_u8, n_mine, frame_u8, W, H, n, rank, spp_total):
+    """The timed job is complete: every pixel of the rank's shard took every sample, and on rank 0
+    the gathered frame is complete and equal to rank 0's shard where they overlap."""
+    mine = shard_u8[: n_mine * 40].view(L.PIXEL_STATS_DTYPE)
+    assert int(mine["n"].min()) == spp_total and int(mine["n"].max()) == spp_total, "every pixel must take every sample"
+    if rank == 0:
+        fr = frame_u8.view(L.PIXEL_STATS_DTYPE)
+        assert int(fr["n"].min()) == spp_total and int(fr["n"].max()) == spp_total, "gathered frame incomplete"
+        assert np.array_equal(fr[shard.tile_pixels(W, H, 0, n)].view(np.uint8).reshape(-1), shard_u8[: n_mine * 40]), \
+            "gathered frame differs from rank 0's shard"
+
+
+def timed_region(ctl, steps, step, gather, sync):
+    """K steps plus the gather, bracketed by a barrier + device synchronisation on both sides;
+    -> the max over ranks of the wall time."""
+    ctl.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    gather()
+    sync()
+    ctl.barrier()
+    return ctl.max(time.perf_counter() - t0)
+
+
+class HostComm:
+    """--host-rehearsal only (tests/test_bench_cpu.py): a stand-in for shard.Comm over the gloo
+    group, so that bench.py's N>1 control flow -- unique-id hand-off, RCCL's rank check, the spp
+    split, shard capacities, the timed region's barriers and max, the gather into rank 0 and the
+    checks on the gathered frame -- runs on CPU processes.  It renders nothing: a step adds its
+    samples to every pixel of the shard with a pixel-keyed sum, and the gather moves the host
+    shards to rank 0 and places them with the product's own om_shard_assemble_host."""
+
+    def __init__(self, uid):
+        assert len(uid) == L.OM_COMM_ID_BYTES
+        self.n = dist.get_world_size() if dist.is_initialized() else 1
+        self.rank = dist.get_rank() if dist.is_initialized() else 0
+
+    def info(self):
+        return self.n, self.rank
+
+    def render_shard(self, pixels, shard_arr, spp):
+        st = shard_arr[: pixels.size]
+        st["n"] += spp
+        st["sum"] += (pixels.astype(np.float32) * spp)[:, None]
+
+    def gather_frame(self, shard_arr, W, H):
+        shards = [None] * self.n if self.rank == 0 else None
+        if self.n > 1:
+            dist.gather_object(shard_arr.view(np.uint8), shards, dst=0)
+        else:
+            shards = [shard_arr.view(np.uint8)]
+        return shard.assemble(W, H, shards).view(np.uint8) if self.rank == 0 else np.zeros(40, np.uint8)
+
+
+def run_host_rehearsal(name, ctl, steps, warmup, spp_per_step):
+    """bench.py's N>1 harness on CPU processes (--host-rehearsal, gloo): the run_config control flow
+    with HostComm in place of RCCL and no device.  Returns the fields run_config returns (the
+    roofline, work and window parity are device measurements: None)."""
+    n, rank = ctl.n, ctl.rank
+    comm = HostComm(ctl.unique_id())
+    nranks_seen = check_comm_ranks(comm.info(), n, rank)
+    W, H, depth, spp_step, spp_total, cap, n_mine = layout(name, n, rank, spp_per_step, steps)
+    pixels = shard.tile_pixels(W, H, rank, n)
+    sh = np.zeros(cap, dtype=L.PIXEL_STATS_DTYPE)
+    for _ in range(warmup):
+        comm.render_shard(pixels, sh, spp_step)
+    sh[:] = 0
+    out = {}
+    elapsed = timed_region(ctl, steps, lambda i: comm.render_shard(pixels, sh, spp_step),
+                           lambda: out.__setitem__("frame", comm.gather_frame(sh, W, H)), lambda: None)
+    check_gathered(sh.view(np.uint8), n_mine, out["frame"], W, H, n, rank, spp_total)
+    if rank == 0:
+        fr = out["frame"].view(L.PIXEL_STATS_DTYPE)
+        assert np.array_equal(fr["sum"][:, 0], np.arange(W * H, dtype=np.float32) * spp_total), "pixels misplaced"
+    return {"value": round(W * H * spp_total / elapsed / 1e6, 3), "elapsed_s": elapsed, "steps": steps, "W": W, "H": H,
+            "depth": depth, "spp_total": spp_total, "spp_step": spp_step, "mega": False, "roofline": None,
+            "window_parity": None, "nranks_seen": nranks_seen, "work": None, "shard_capacity": cap, "shard_pixels": n_mine}
+
+
+def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_mode, pmc_ok=True):
+    """One config through the product path; returns the measured fields (value, roofline, work)."""
+    if args.host_rehearsal:
+        return run_host_rehearsal(name, ctl, steps, warmup, spp_per_step)
+    cfg = CONFIGS[name]
     n, rank = ctl.n, ctl.rank
     # a dedicated (non-NULL) stream: the kernels, their HIP events and the RCCL gather run on it
     stream = torch.cuda.Stream()
@@ -217,6 +311,7 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
     sptr = stream.cuda_stream
     assert sptr, "need a non-default stream handle"
     world = make_scene(cfg["scene"], om)
+    W, H = cfg.get("size", (1920, 1080))
     cam = om.default_camera(W / H)
     frozen = world.freeze(cam, device=local_rank, kernel=args.kernel, pipeline=args.pipeline)
     ctx = frozen.ctx
@@ -225,10 +320,7 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
     L.check(L.lib.om_set_primary_lists(ctx, {"off": 0, "auto": 1, "on": 2}[args.primary_lists]), ctx)
     comm = shard.Comm(ctx, n, rank, ctl.unique_id())
     nranks_seen = check_comm_ranks(comm.info(), n, rank)     # RCCL's own view of the communicator
-    spp_step = spp_per_step * (1 if name == "C4" else n)          # C4: fixed frame; else fixed per-GPU work
-    spp_total = spp_step * steps
-    cap = shard.shard_capacity(W, H, n)
-    n_mine = shard.tile_pixels(W, H, rank, n).size
+    W, H, depth, spp_step, spp_total, cap, n_mine = layout(name, n, rank, spp_per_step, steps)
     sh = torch.zeros(cap * 40, dtype=torch.uint8, device="cuda")
     frame = torch.zeros((W * H if rank == 0 else 1) * 40, dtype=torch.uint8, device="cuda")
     p = om.make_params(depth, TMIN, TMAX, spp_total, W, H, sample_count=spp_step, seed=SEED,
@@ -253,35 +345,26 @@ def run_config(name, args, ctl, local_rank, steps, warmup, spp_per_step, timing_
     L.check(L.lib.om_set_timing(ctx, {"off": 0, "region": 0, "launch": 1, "span": 2}[timing_mode]), ctx)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
-    # ---- timed region
-    ctl.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(steps):
+    # ---- timed region: ev0 before the first call, ev1 after the last, then the gather
+    def timed_step(i):
+        if i == 0:
+            ev0.record(stream)
         step()
-    ev1.record(stream)
-    comm.gather_frame(sh.data_ptr(), W, H, frame.data_ptr(), sptr)   # RCCL: every shard to rank 0
-    torch.cuda.synchronize()
-    ctl.barrier()
-    elapsed = time.perf_counter() - t0
-    # ---- end timed region
 
-    elapsed = ctl.max(elapsed)
+    def gather():
+        ev1.record(stream)
+        comm.gather_frame(sh.data_ptr(), W, H, frame.data_ptr(), sptr)   # RCCL: every shard to rank 0
+    elapsed = timed_region(ctl, steps, timed_step, gather, torch.cuda.synchronize)
+    # ---- end timed region
     region_s = ev0.elapsed_time(ev1) / 1e3                    # device time of the K calls
     L.check(L.lib.om_get_kernel_times(ctx, C.byref(kt)), ctx)
     L.check(L.lib.om_set_timing(ctx, 0), ctx)
     host = sh.cpu().numpy().copy()
-    mine = host[: n_mine * 40].view(L.PIXEL_STATS_DTYPE)
-    assert int(mine["n"].min()) == spp_total and int(mine["n"].max()) == spp_total, "every pixel must take every sample"
+    frame_u8 = frame.cpu().numpy()
+    check_gathered(host, n_mine, frame_u8, W, H, n, rank, spp_total)
     parity = None
-    if rank == 0:
-        fr = frame.cpu().numpy().view(L.PIXEL_STATS_DTYPE)
-        assert int(fr["n"].min()) == spp_total and int(fr["n"].max()) == spp_total, "gathered frame incomplete"
-        assert np.array_equal(fr[shard.tile_pixels(W, H, 0, n)].view(np.uint8).reshape(-1), host[: n_mine * 40]), \
-            "gathered frame differs from rank 0's shard"
-        if not args.no_window_parity:
-            parity = window_parity(name, fr.view(np.uint8), W, H, spp_total, depth, cfg["march_steps"])
+    if rank == 0 and not args.no_window_parity:
+        parity = window_parity(name, frame_u8, W, H, spp_total, depth, cfg["march_steps"])
 
     # per-launch durations (untimed): the same K steps again, production build, every launch
     # bracketed by events on its stream (om_set_timing 1) -> the rocprof-comparable average
@@ -421,6 +504,9 @@ def main():
                     help="quick mode: the headline config only (no CPU baselines, no `configs` block)")
     ap.add_argument("--no-extras", action="store_true", help="no `configs` block (C2/C3/C0) at N=1")
     ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--host-rehearsal", action="store_true",
+                    help="tests only: run the N>1 control flow on CPU processes (gloo), RCCL replaced by HostComm; "
+                         "renders nothing, prints no measurement")
     ap.add_argument("--no-window-parity", action="store_true",
                     help="skip the oracle window of each timed frame (untimed; a few seconds of host CPU)")
     args = ap.parse_args()
@@ -431,12 +517,20 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
-    torch.cuda.set_device(local_rank)
+    if not args.host_rehearsal:
+        torch.cuda.set_device(local_rank)
     ctl = Control(world_size, rank)
     steps = args.steps
     if steps is None:
         steps = cfg["spp"] // args.spp_per_step if args.config != "C4" else cfg["spp"] // args.spp_per_step
     r = run_config(args.config, args, ctl, local_rank, steps, args.warmup, args.spp_per_step, args.kernel_timing)
+    if args.host_rehearsal:                  # no device ran: a rehearsal record, never a metric line
+        if rank == 0:
+            print(json.dumps({"host_rehearsal": True, "config": args.config, "n_ranks": world_size, "steps": steps,
+                              **{k: r[k] for k in ("spp_step", "spp_total", "W", "H", "nranks_seen", "shard_capacity",
+                                                   "shard_pixels", "elapsed_s")}}))
+        ctl.close()
+        return
 
     extras = None
     quick = args.no_cpu_baseline or args.no_extras

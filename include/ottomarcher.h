@@ -300,7 +300,9 @@ om_status om_set_streams(om_ctx* ctx, uint32_t streams);
  * batch renders b samples of every listed pixel: enough for 2^paths_log2 paths (0 = default 22),
  * at least an even share of the call's remaining samples over the batches left, at most the
  * remainder; samples past a pixel's retirement inside a batch are dropped in sample order.  A
- * pure scheduling knob: results are bit-identical for every value. */
+ * pure scheduling knob: results are bit-identical for every value.  batches <= 64: the host never
+ * reads the live count back, so every planned batch is launched even once the plan leaves it no
+ * pixel (a bounce chain plus an accumulate per stream, ~5 us per launch that returns at once). */
 om_status om_set_adaptive_batches(om_ctx* ctx, uint32_t batches, uint32_t paths_log2);
 
 /* Primary rays (wavefront, BVH2): bounce 0 can test, per 8x8 pixel tile, only the leaf

@@ -272,12 +272,38 @@ void build_skip_bvh(const om_world& w, FrozenWorld& fw) {
     fw.srecs.clear();
     if (b.items.empty()) return;
     uint32_t root = b.build(0, (uint32_t)b.items.size());
-    size_t internal = 0, leaves = 0;
-    for (const OmBvhNode& n : b.nodes) (n.left < 0 ? leaves : internal) += 1;
+    // internal nodes, leaves, and internal nodes on the deepest root-to-leaf path (the compressed
+    // tree's lane-stack bound, fw.b2_depth below) of the built tree
+    auto tree_stats = [&](uint32_t r, size_t& internal, size_t& leaves, uint32_t& tdepth) {
+        internal = 0; leaves = 0; tdepth = 0;
+        std::vector<std::pair<uint32_t, uint32_t>> st{{r, 1u}};
+        while (!st.empty()) {
+            const auto [n, d] = st.back();
+            st.pop_back();
+            const OmBvhNode& nd = b.nodes[n];
+            if (nd.left < 0) { ++leaves; continue; }
+            ++internal; tdepth = std::max(tdepth, d);
+            st.push_back({(uint32_t)nd.left, d + 1u}); st.push_back({(uint32_t)nd.right, d + 1u});
+        }
+    };
+    size_t internal, leaves;
+    uint32_t tdepth;
+    tree_stats(root, internal, leaves, tdepth);
     if (internal * sizeof(OmBvh2Node) + leaves * 4u > kB2LdsBudget) {    // read through L2: smaller leaves
-        b.nodes.clear(); b.order.clear();
+        std::vector<OmBvhNode> nodes8;
+        std::vector<uint32_t> order8;
+        nodes8.swap(b.nodes); order8.swap(b.order);
+        const uint32_t root8 = root;
         b.max_leaf = OM_BVH_MAX_LEAF_L2; b.leaf_force = OM_BVH_LEAF_FORCE_L2;
         root = b.build(0, (uint32_t)b.items.size());
+        tree_stats(root, internal, leaves, tdepth);
+        // the compressed BVH2 needs 15-bit node and leaf codes and a lane stack of <= 24 entries
+        // (om_upload_world's b2_ok): one record per leaf gives one leaf per bounded primitive, which
+        // breaks those limits from ~32k primitives on -- keep the max-leaf tree then
+        if (!(internal < 32768u && leaves < 32768u && tdepth <= 24u)) {
+            b.nodes.swap(nodes8); b.order.swap(order8);
+            root = root8;
+        }
     }
     // depth-first re-emission with skip links
     std::vector<uint32_t> leaf_first(b.nodes.size(), 0);

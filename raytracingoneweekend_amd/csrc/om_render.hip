@@ -764,8 +764,11 @@ om_status om_set_streams(om_ctx* c, uint32_t streams) {
 
 om_status om_set_adaptive_batches(om_ctx* c, uint32_t batches, uint32_t paths_log2) {
     if (!c) return set_err(nullptr, OM_ERR_INVALID, "null ctx");
-    if (batches > 4096u || paths_log2 > 27u)
-        return set_err(c, OM_ERR_INVALID, "om_set_adaptive_batches: batches <= 4096, paths_log2 <= 27");
+    // every planned batch is launched whether or not the device plan leaves it any pixel (the host
+    // never reads the live count back): ~10 launches of ~5 us each per empty batch and stream, so
+    // the knob is capped at a few dozen batches
+    if (batches > 64u || paths_log2 > 27u)
+        return set_err(c, OM_ERR_INVALID, "om_set_adaptive_batches: batches <= 64, paths_log2 <= 27");
     c->ad_batches = batches; c->ad_paths_log2 = paths_log2;
     return OM_OK;
 }

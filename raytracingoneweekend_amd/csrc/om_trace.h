@@ -670,7 +670,11 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
 
 // HYB: only nodes [0, nl) are in `nodes` (the breadth-first prefix staged in LDS); the
 // others are read from `gnodes` (global memory, through L2).
-template <int DEPTH, int STRIDE, class Wk, bool HYB = false, class Node = OmBvh2Node>
+// NSTRIDE: bytes between consecutive nodes of `nodes` (padded in LDS to spread the bank slots).
+// (Pop culling -- u32 entries carrying the pushed child's near distance, popped entries beyond
+// the current closest dropped unread -- removed only 1.8% of the box tests on C1 and cost LDS
+// occupancy on C3: DESIGN.md §8, r06.)
+template <int DEPTH, int STRIDE, class Wk, bool HYB = false, class Node = OmBvh2Node, int NSTRIDE = (int)sizeof(Node)>
 __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* nodes, const uint32_t* leaves,
                                            const OmAffineTest* recs, uint16_t* stk,
                                            F3 o, F3 d, float tmin, float& closest, Wk& w,
@@ -702,6 +706,13 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
     };
     uint32_t cur = 0;                                   // 16-bit code: node index | OM_LEAF + leaf index
     int sp = 0;                                         // lane stack: one entry per internal level
+    // next entry off the stack -> cur; false when the stack is empty
+    auto pop = [&]() -> bool {
+        if (sp == 0) return false;
+        --sp;
+        cur = stk[sp * STRIDE];
+        return true;
+    };
     // the leaf and node steps of one loop, each ending in `continue`: the structurizer turns
     // this shape into a node loop nested in the leaf loop (a lane descends until it reaches a
     // leaf, then the wave's leaves are tested) -- written as one flat if/else loop instead,
@@ -709,12 +720,10 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
     for (;;) {
         if (cur >= OM_LEAF) {                       // the single leaf site (16-bit codes: one compare, no and)
             test_leaf(recs, leaf_payload(S, cur, leaves), o, d, tmin, closest, best, w);
-            if (sp == 0) break;
-            --sp;
-            cur = stk[sp * STRIDE];
+            if (!pop()) break;
             continue;
         }
-        const Node N = (HYB && cur >= nl) ? gnodes[cur] : nodes[cur];
+        const Node N = (HYB && cur >= nl) ? gnodes[cur] : *(const Node*)((const char*)nodes + cur * (uint32_t)NSTRIDE);
         bool h0, h1, swap;
         slabs(N, h0, h1, swap);
         if (h0 && h1) {                             // near child next, far child pushed
@@ -724,9 +733,7 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
         } else if (h0 || h1) {
             cur = h0 ? N.c0 : N.c1;
         } else {
-            if (sp == 0) break;
-            --sp;
-            cur = stk[sp * STRIDE];
+            if (!pop()) break;
             continue;
         }
     }
@@ -777,7 +784,9 @@ __device__ __forceinline__ int traced_bvh4(const OmSceneDev& S, const Node* node
             const float tf = slab_far(x0, x1, y0, y1, z0, z1, t_hi);
             const uint32_t c = N.child[k];
             const bool h = !(tn > tf) && c != OM_EMPTY;
-            key[k] = h ? tn : INFINITY;
+            // a NaN slab counts as a hit but sorts by t_lo: the network needs ordered keys (a NaN
+            // key compares false both ways and could leave a missed child ahead of the hit one)
+            key[k] = h ? fmaxf(tn, t_lo) : INFINITY;
             code[k] = c;
             n += h ? 1 : 0;
         }

@@ -107,3 +107,10 @@
 #ifndef OM_ACC_GROUP
 #define OM_ACC_GROUP 8
 #endif
+// BVH2 f32 nodes staged whole in LDS: bytes between consecutive nodes (64 = packed).  A wave's
+// node reads are ds_read_b128/b96 at random nodes; at a 64-B stride word k of every node falls
+// in one of 4 (b128) / 2 (b96) bank slots, at 80 B in one of 16 / 8 (r06, VERDICT r05 #1b).
+// C1 (r06_ab1, r06_ab2): 80 -> 7128, 7118 / 6902, 6911 vs 64 -> 7077, 7107 / 6863, 6874 Msamples/s.
+#ifndef OM_B2_NODE_STRIDE
+#define OM_B2_NODE_STRIDE 80
+#endif

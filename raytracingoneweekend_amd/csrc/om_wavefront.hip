@@ -63,12 +63,19 @@ enum { TR_BRUTE = 1, TR_CULLED = 2, TR_BVH = 3, TR_SBVH_LDS = 4, TR_SBVH_GLOBAL 
        TR_BVH4_LDS = 8, TR_BVH4_GLOBAL = 9 };
 #define OM_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(OM_WF_WAVES, OM_WF_WAVES)))   // occupancy request (waves per SIMD)
 constexpr int kBlk = OM_WF_BLOCK;                                 // workgroup = one queue segment
-constexpr int kStackDepth = 24;                                   // BVH2 per-lane LDS stack bound (u16 entries)
+constexpr int kStackDepth = 24;                                   // BVH2 per-lane LDS stack bound (entries)
+// f32 BVH2 nodes staged in LDS sit OM_B2_NODE_STRIDE bytes apart (om_tuning.h)
+constexpr uint32_t kB2Stride = OM_B2_NODE_STRIDE;
+static_assert(kB2Stride % 16u == 0u && kB2Stride >= sizeof(OmBvh2Node), "16-B aligned node slots");
 // LDS bytes of the lane stack: S.b2_stack entries per lane (the tree's internal depth, 9 for
 // S-traced: 9 KiB per 512-lane workgroup instead of 24 KiB at the 24-entry bound).
 template <int TR>
 __host__ __device__ inline uint32_t stack_bytes(const OmSceneDev& S) {
     return kBlk * ((TR == TR_BVH4_LDS || TR == TR_BVH4_GLOBAL) ? S.b4_stack : S.b2_stack) * 2u;
+}
+// LDS bytes of a BVH2 staged whole (TR_BVH2_LDS): padded nodes + leaf table
+__host__ __device__ inline uint32_t b2_stage_bytes(const OmSceneDev& S) {
+    return (S.n_b2nodes * kB2Stride + S.n_b2leaves * 4u + 15u) & ~15u;
 }
 constexpr uint32_t kTailSpb = OM_WF_TAIL_SPB;                     // queue segments per tail workgroup
 constexpr uint32_t kTailDefault = 16;                             // first bounce handled by the tail kernel
@@ -253,12 +260,14 @@ __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every 
         t.h2l = (const OmBvh2NodeH*)dst;
     }
     if (TR == TR_BVH2_LDS || TR == TR_BVH4_LDS) {
-        const uint32_t nn = TR == TR_BVH2_LDS ? S.n_b2nodes * (uint32_t)(sizeof(OmBvh2Node) / 16u)
-                                              : S.n_b4nodes * (uint32_t)(sizeof(OmBvh4Node) / 16u);   // uint4 per node
+        // uint4 words per node in memory / per node slot in LDS (BVH2: padded to kB2Stride)
+        constexpr uint32_t wn = TR == TR_BVH2_LDS ? (uint32_t)(sizeof(OmBvh2Node) / 16u) : (uint32_t)(sizeof(OmBvh4Node) / 16u);
+        constexpr uint32_t ws = TR == TR_BVH2_LDS ? kB2Stride / 16u : wn;
+        const uint32_t nn = (TR == TR_BVH2_LDS ? S.n_b2nodes : S.n_b4nodes) * wn;
         const uint4* sn = TR == TR_BVH2_LDS ? (const uint4*)S.b2nodes : (const uint4*)S.b4nodes;
         uint4* dst = wf_lds + STACKS * stack_bytes<TR>(S) / 16u;
-        for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[i] = sn[i];
-        uint32_t* ldst = (uint32_t*)(dst + nn);
+        for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[(i / wn) * ws + i % wn] = sn[i];
+        uint32_t* ldst = (uint32_t*)(dst + nn / wn * ws);
         for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += kBlk) ldst[i] = S.b2leaves[i];
         __syncthreads();
         t.b2n = (const OmBvh2Node*)dst; t.b4n = (const OmBvh4Node*)dst; t.bl = ldst;
@@ -277,7 +286,8 @@ __device__ __forceinline__ int trace(const OmSceneDev& S, const OmParamsDev& P, 
     if (TR == TR_BVH4_LDS) best = traced_bvh4<kBlk>(S, T.b4n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
     else if (TR == TR_BVH4_GLOBAL)
         best = traced_bvh4<kBlk, Wk, true>(S, T.h4l, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w, T.h4g, T.nl);
-    else if (TR == TR_BVH2_LDS) best = traced_bvh2<kStackDepth, kBlk>(S, T.b2n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
+    else if (TR == TR_BVH2_LDS)
+        best = traced_bvh2<kStackDepth, kBlk, Wk, false, OmBvh2Node, (int)kB2Stride>(S, T.b2n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
     else if (TR == TR_BVH2_GLOBAL)
         best = traced_bvh2<kStackDepth, kBlk, Wk, true>(S, T.h2l, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w, T.h2g, T.nl);
     else if (TR == TR_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);
@@ -1074,7 +1084,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     const uint32_t segcap = seg_capacity(max_paths, nseg);
     hipError_t e = grow(B, (uint64_t)nseg * segcap, (depth_cap + 1u) * nseg, (int)ns);
     if (e != hipSuccess) { err = "wavefront buffer allocation failed"; return e; }
-    const uint32_t lds = tr == TR_BVH2_LDS ? stack_bytes<TR_BVH2_LDS>(L.S) + L.S.b2_lds_bytes
+    const uint32_t lds = tr == TR_BVH2_LDS ? stack_bytes<TR_BVH2_LDS>(L.S) + b2_stage_bytes(L.S)
                        : tr == TR_BVH2_GLOBAL ? stack_bytes<TR_BVH2_GLOBAL>(L.S) + hyb_nodes(L.S) * (uint32_t)sizeof(OmBvh2NodeH)
                        : tr == TR_BVH4_LDS ? stack_bytes<TR_BVH4_LDS>(L.S) + L.S.b4_lds_bytes
                        : tr == TR_BVH4_GLOBAL ? stack_bytes<TR_BVH4_GLOBAL>(L.S) + hyb4_nodes(L.S) * (uint32_t)sizeof(OmBvh4NodeH)

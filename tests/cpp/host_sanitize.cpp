@@ -147,6 +147,20 @@ int main() {
         std::printf("%s: %u prims, %zu BVH2 nodes, %zu tile-list entries\n", sc.name, fw.offsets[8], fw.b2nodes.size(), lists);
         om_world_destroy(w);
     }
+    // a field of 40k spheres: one record per leaf would give ~40k leaves, past the compressed
+    // BVH2's 15-bit codes, so the builder must keep a tree om_upload_world accepts
+    {
+        om_world* w = nullptr;
+        EXPECT(om_world_create(&w) == OM_OK);
+        EXPECT(om_world_random_scene(w, 0x5EED, 2u, 100) == OM_OK);
+        om::FrozenWorld fw;
+        w->freeze(fw);
+        EXPECT(fw.offsets[8] >= 39000u);
+        EXPECT(!fw.b2nodes.empty() && fw.b2nodes.size() < 32768u && fw.b2leaves.size() < 32768u && fw.b2_depth <= 24u);
+        std::printf("S-40k: %u prims, %zu BVH2 nodes, %zu leaves, depth %u\n", fw.offsets[8], fw.b2nodes.size(),
+                    fw.b2leaves.size(), fw.b2_depth);
+        om_world_destroy(w);
+    }
     // the tile deal of the multi-GPU path (om_multi.hip host side)
     for (uint32_t n : {1u, 2u, 3u, 8u}) {
         const uint32_t W = 37, H = 21, cap = om_shard_capacity(W, H, n);

@@ -391,7 +391,8 @@ def test_concurrent_adaptive_batches_are_bit_identical(om, oracle, streams, sche
         nb, msg = compare_stats(pix.pixels, exp, f"adaptive streams{streams} sched{sched} calls{counts}")
         assert nb == 0, msg
         assert int(pix.pixels["n"].min()) < SPP
-    assert L.lib.om_set_adaptive_batches(fz.ctx, 5000, 0) == L.OM_ERR_INVALID
+    assert L.lib.om_set_adaptive_batches(fz.ctx, 65, 0) == L.OM_ERR_INVALID
+    assert L.lib.om_set_adaptive_batches(fz.ctx, 64, 0) == L.OM_OK
     assert L.lib.om_set_adaptive_batches(fz.ctx, 0, 28) == L.OM_ERR_INVALID
 
 

@@ -84,6 +84,9 @@ declare -A V=(
   [bl2t05]="$COMMON $DEV -DOM_BVH_MAX_LEAF=2 -DOM_BVH_TRAV=0.5"
   [bt05]="$COMMON $DEV -DOM_BVH_TRAV=0.5"
   [bt2]="$COMMON $DEV -DOM_BVH_TRAV=2.0"
+  # r06: BVH2 f32 LDS node stride (bank slots; default 80)
+  [p64]="$COMMON $DEV -DOM_B2_NODE_STRIDE=64"
+  [p96]="$COMMON $DEV -DOM_B2_NODE_STRIDE=96"
   # LLVM AMDGPU scheduler strategies (same code, different instruction order)
   [ilp]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-ilp"
   [memclause]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-memory-clause"
