@@ -1,4 +1,4 @@
-"""Print the (variant, value, ms/step, march steps/segment) rows of a tools/ab.sh result file."""
+"""Print the (variant, value, ms/step, march steps/segment) rows of a tools/ab_run.sh / tools/sweep.sh result file."""
 import json
 import sys
 
