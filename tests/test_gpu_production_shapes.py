@@ -148,14 +148,18 @@ def test_c3_shape_1080p_10k_bvh2_l2(om, oracle):
 
 
 def test_c2_shape_1080p_marched_split_pipeline(om, oracle):
-    """C2: 1080p S-marched (256 march steps) on the split march pipeline (k_raygen + lane-refilling
-    k_march + k_bounce<HIT>, tail 12), one 16-spp call == 16 one-spp calls == oracle windows."""
+    """C2: 1080p S-marched (256 march steps) on the split march pipeline: bounce 0 as k_raygen +
+    lane-refilling k_march + k_bounce<HIT>, every later segment in the lane-refilling marched tail
+    (from bounce 1, om_tuning.h OM_WF_TAIL_MARCHED); one 16-spp call == 16 one-spp calls == oracle
+    windows."""
     W, H, SPP, STEPS = 1920, 1080, 16, 256
     world = _scene(om, "S-marched")
     cam = om.default_camera(W / H)
     fz = world.freeze(cam)
     big, kt = _render_calls(om, fz, cam, W, H, SPP, SPP, STEPS, timing=True)
     assert _launches(kt, "megakernel") == 0 and _launches(kt, "tail") == 2, "expected the wavefront, 2 batches"
+    # per batch: k_raygen + k_march + k_bounce<HIT> (bounce 0), no per-bounce launch after it
+    assert _launches(kt, "bounce0") == 6 and _launches(kt, "bounce") == 0, "expected the marched tail from bounce 1"
     small, _ = _render_calls(om, fz, cam, W, H, SPP, 1, STEPS)
     fz.close()
     diff = int((big != small).view(-1, 40).any(1).sum())
