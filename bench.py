@@ -517,6 +517,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world_size != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world_size}")
+    if world_size > 1 and int(os.environ.get("LOCAL_WORLD_SIZE", world_size)) == world_size:
+        # one node: RCCL's bootstrap (the unique id rank 0 hands out) over loopback, whatever the
+        # container's hostname and interfaces; the frame data goes over xGMI, not sockets
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     if not args.host_rehearsal:
         torch.cuda.set_device(local_rank)
     ctl = Control(world_size, rank)
