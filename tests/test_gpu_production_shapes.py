@@ -98,6 +98,25 @@ def test_c4_shape_4k_32spp_one_call(om, oracle):
     _check_windows(oracle, "S-traced", big.cpu().numpy(), W, H, SPP, 24, 1024)
 
 
+def test_max_frame_8k_one_call(om, oracle):
+    """The largest frame the bench family reaches, and then some: 7680x4320 (33.2 M pixels, 4x C4),
+    one 4-spp call = two concurrent 2-spp batches of 66 M paths (the 2^27-path cap on a batch
+    decides the split; above 2^25 paths: tail from bounce 24) == 4 one-spp calls == oracle windows.
+    Path slots, pixel indices and queue offsets stay 32-bit clean at this size."""
+    W, H, SPP = 7680, 4320, 4
+    world = _scene(om, "S-traced")
+    cam = om.default_camera(W / H)
+    fz = world.freeze(cam)
+    big, kt = _render_calls(om, fz, cam, W, H, SPP, SPP, 1024, timing=True)
+    assert _launches(kt, "bounce0") == 2 and _launches(kt, "tail") == 2, "expected two concurrent 2-spp batches"
+    assert _launches(kt, "bounce") == 2 * 23, "expected the big-batch tail threshold (24)"
+    small, _ = _render_calls(om, fz, cam, W, H, SPP, 1, 1024)
+    fz.close()
+    diff = int((big != small).view(-1, 40).any(1).sum())
+    assert diff == 0, f"{diff} pixels differ between the 4-spp call and 4 one-spp calls"
+    _check_windows(oracle, "S-traced", big.cpu().numpy(), W, H, SPP, 16, 1024)
+
+
 def test_c1_shape_1080p_128spp_shard_call(om, oracle):
     """C1: bench.py's step itself -- om_render_shard of 128 spp over the (N=1) tile shard, eight
     16-spp batches of 33 M paths on two streams, then the RCCL gather -- == 128 one-spp calls

@@ -19,3 +19,16 @@ def test_host_code_under_asan_ubsan():
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-6000:]
     assert "sanitize ok" in r.stdout
     assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-6000:]
+
+
+def test_packet_traversal_would_visit_more_than_the_busiest_lane():
+    """DESIGN.md §8 (VERDICT r05 #1c): on the product's S-traced BVH2, the bounce-1 rays of an 8x8
+    tile need more node and leaf visits as a packet (the union) than the busiest lane of the
+    shipped per-ray traversal (tests/cpp/packet_union.cpp, host code only)."""
+    import re
+    subprocess.check_call(["make", "-s", "-C", CPP, "packet_union"])
+    out = subprocess.run([os.path.join(CPP, "packet_union")], capture_output=True, text=True, timeout=120, check=True).stdout
+    m = re.search(r"per ray ([\d.]+), busiest lane ([\d.]+), packet union ([\d.]+); leaf visits busiest lane ([\d.]+), "
+                  r"packet union ([\d.]+)", out)
+    per_ray, lane, union, leaf_lane, leaf_union = map(float, m.groups())
+    assert union > 1.2 * lane and leaf_union > 1.5 * leaf_lane and lane > per_ray, out
