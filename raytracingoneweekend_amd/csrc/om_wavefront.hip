@@ -763,7 +763,7 @@ void k_tail(OmSceneDev S, OmParamsDev P, Seg G, Queue in,
 // ---------------------------------------------------------------- accumulate
 // Adaptive batches (ad.list): lane kk owns live-list entry kk, and a pixel that is still live after
 // the batch, with samples of the call left, is appended to the stream's next list (one ballot and
-// one atomic per wave: ThreadPixels::add_run / swap_buffers, render_thread.rs:68-102).  The list's
+// one atomic per workgroup: ThreadPixels::add_run / swap_buffers, render_thread.rs:68-102).  The list's
 // order then depends on which wave appends first; a result's slot and a path's RNG never do.
 template <bool COUNT>
 __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_stats* __restrict__ stats,
@@ -831,15 +831,33 @@ __global__ __launch_bounds__(kBlk) void k_accumulate(OmParamsDev P, om_pixel_sta
     if (ad.list) {                                                  // the stream's next live list
         const uint64_t m = __ballot(relist);
         uint32_t base = 0u;
-        if (__lane_id() == 0 && m) base = atomicAdd(&ad.plan_next->c, (uint32_t)__popcll(m));
-        base = __builtin_amdgcn_readfirstlane(base);
+        // one global atomic per workgroup (the waves' counts summed in LDS first): the ~16k
+        // contended atomics on one word of a 1M-pixel accumulate become ~2k (r06: C1_adaptive
+        // +3.8%, profiles/r06_adaptive)
+        __shared__ uint32_t wg_n, wg_base;
+        if (threadIdx.x == 0) wg_n = 0u;
+        __syncthreads();
+        if (__lane_id() == 0 && m) base = atomicAdd(&wg_n, (uint32_t)__popcll(m));
+        __syncthreads();
+        if (threadIdx.x == 0) wg_base = wg_n ? atomicAdd(&ad.plan_next->c, wg_n) : 0u;
+        __syncthreads();
+        base = __builtin_amdgcn_readfirstlane(base) + wg_base;
         if (relist) ad.list_next[base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull))] = k;
     }
     if (COUNT) {
         flush_counter(counters, OMC_SAMPLES, n_samples);
         flush_counter(counters, OMC_CREDITED, credited);
     }
-    if (P.progress) flush_counter(counters, OMC_PROGRESS, credited);      // live samples_atom (om_progress)
+    if (P.progress) {                                               // live samples_atom (om_progress)
+        // summed per workgroup first: one contended atomic per workgroup, not per wave
+        __shared__ unsigned long long wg_credit;
+        if (threadIdx.x == 0) wg_credit = 0ull;
+        __syncthreads();
+        const uint32_t v = wave_sum32(credited);
+        if (__lane_id() == 0 && v) atomicAdd(&wg_credit, (unsigned long long)v);
+        __syncthreads();
+        if (threadIdx.x == 0 && wg_credit) atomicAdd(&counters[OMC_PROGRESS], wg_credit);
+    }
 }
 
 // k_snapshot: n0[k] = Stats.n of listed pixel k at the start of a concurrent fixed-spp call.
@@ -852,13 +870,14 @@ __global__ __launch_bounds__(256) void k_snapshot(const om_pixel_stats* __restri
 
 // k_ad_init: the first live list of every stream of an adaptive call.  Chunk q of 64 list entries
 // (a tile of a frame list) belongs to stream q % ns; its pixels that are not retired and have
-// samples left are appended to that stream's list (one ballot + one atomic per wave: a wave is one
+// samples left are appended to that stream's list (one ballot per wave, one atomic per workgroup and stream: a wave is one
 // chunk).  plans (zeroed by the caller) get the counts.
-__global__ __launch_bounds__(256) void k_ad_init(const om_pixel_stats* __restrict__ stats, const uint32_t* __restrict__ pixels,
+constexpr uint32_t kAdInitBlk = 1024u;
+__global__ __launch_bounds__(kAdInitBlk) void k_ad_init(const om_pixel_stats* __restrict__ stats, const uint32_t* __restrict__ pixels,
                                                  uint32_t n_pixels, uint32_t by_pixel, uint32_t spp_total, uint32_t ns,
                                                  uint32_t* __restrict__ lists, uint64_t list_stride, AdPlan* __restrict__ plans,
                                                  uint32_t plan_stride) {
-    const uint32_t k = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t k = blockIdx.x * kAdInitBlk + threadIdx.x;
     bool live = false;
     if (k < n_pixels) {
         const om_pixel_stats& ps = stats[by_pixel ? pixels[k] : k];
@@ -867,8 +886,16 @@ __global__ __launch_bounds__(256) void k_ad_init(const om_pixel_stats* __restric
     const uint32_t s = (k >> 6) % ns;                                // wave-uniform
     const uint64_t m = __ballot(live);
     uint32_t base = 0u;
-    if (__lane_id() == 0 && m) base = atomicAdd(&plans[(uint64_t)s * plan_stride].c, (uint32_t)__popcll(m));
-    base = __builtin_amdgcn_readfirstlane(base);
+    // per stream, one global atomic per workgroup (the waves' counts summed in LDS first)
+    __shared__ uint32_t wg_n[4], wg_base[4];
+    if (threadIdx.x < 4u) wg_n[threadIdx.x] = 0u;
+    __syncthreads();
+    if (__lane_id() == 0 && m) base = atomicAdd(&wg_n[s], (uint32_t)__popcll(m));
+    __syncthreads();
+    if (threadIdx.x < ns && wg_n[threadIdx.x])
+        wg_base[threadIdx.x] = atomicAdd(&plans[(uint64_t)threadIdx.x * plan_stride].c, wg_n[threadIdx.x]);
+    __syncthreads();
+    base = __builtin_amdgcn_readfirstlane(base) + (m ? wg_base[s] : 0u);
     if (live) lists[s * list_stride + base + (uint32_t)__popcll(m & ((1ull << __lane_id()) - 1ull))] = k;
 }
 
@@ -1111,7 +1138,7 @@ hipError_t render(Buffers& B, const Launch& L, hipStream_t st, std::string& err)
     AdPlan* plans = adaptive ? (AdPlan*)(B.n0 + (uint64_t)ns * 2u * cmax) : nullptr;
     if (adaptive) {
         (void)hipMemsetAsync(plans, 0, (size_t)ns * plan_stride * sizeof(AdPlan), st);
-        hipLaunchKernelGGL(k_ad_init, dim3((n_px + 255u) / 256u), dim3(256), 0, st, L.stats, L.pixels, n_px, R.by_pixel,
+        hipLaunchKernelGGL(k_ad_init, dim3((n_px + kAdInitBlk - 1u) / kAdInitBlk), dim3(kAdInitBlk), 0, st, L.stats, L.pixels, n_px, R.by_pixel,
                            L.P.spp_total, ns, lists, (uint64_t)2u * cmax, plans, plan_stride);
     } else if (ns > 1) {
         hipLaunchKernelGGL(k_snapshot, dim3((n_px + 255u) / 256u), dim3(256), 0, st, L.stats, L.pixels, n_px, R.by_pixel, B.n0);
