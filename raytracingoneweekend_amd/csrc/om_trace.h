@@ -675,11 +675,13 @@ __device__ __forceinline__ int traced_tiles(const OmSceneDev& S, const uint32_t*
 
 // HYB: only nodes [0, nl) are in `nodes` (the breadth-first prefix staged in LDS); the
 // others are read from `gnodes` (global memory, through L2).
-// NSTRIDE: bytes between consecutive nodes of `nodes` (padded in LDS to spread the bank slots).
+// CUNIT: bytes per unit of an internal node's code: sizeof(Node) when codes are node indices;
+// 16 for the LDS copy at the padded 80-B stride, whose codes stage_scene pre-multiplies (a shift
+// instead of the quarter-rate v_mul_lo_u32 of cur * 80: +0.7% on C1 and C4, r06).
 // (Pop culling -- u32 entries carrying the pushed child's near distance, popped entries beyond
 // the current closest dropped unread -- removed only 1.8% of the box tests on C1 and cost LDS
 // occupancy on C3: DESIGN.md §8, r06.)
-template <int DEPTH, int STRIDE, class Wk, bool HYB = false, class Node = OmBvh2Node, int NSTRIDE = (int)sizeof(Node)>
+template <int DEPTH, int STRIDE, class Wk, bool HYB = false, class Node = OmBvh2Node, int CUNIT = (int)sizeof(Node)>
 __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* nodes, const uint32_t* leaves,
                                            const OmAffineTest* recs, uint16_t* stk,
                                            F3 o, F3 d, float tmin, float& closest, Wk& w,
@@ -728,7 +730,7 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
             if (!pop()) break;
             continue;
         }
-        const Node N = (HYB && cur >= nl) ? gnodes[cur] : *(const Node*)((const char*)nodes + cur * (uint32_t)NSTRIDE);
+        const Node N = (HYB && cur >= nl) ? gnodes[cur] : *(const Node*)((const char*)nodes + cur * (uint32_t)CUNIT);
         bool h0, h1, swap;
         slabs(N, h0, h1, swap);
         if (h0 && h1) {                             // near child next, far child pushed

@@ -266,7 +266,13 @@ __device__ __forceinline__ Tracer stage_scene(const OmSceneDev& S) {   // every 
         const uint32_t nn = (TR == TR_BVH2_LDS ? S.n_b2nodes : S.n_b4nodes) * wn;
         const uint4* sn = TR == TR_BVH2_LDS ? (const uint4*)S.b2nodes : (const uint4*)S.b4nodes;
         uint4* dst = wf_lds + STACKS * stack_bytes<TR>(S) / 16u;
-        for (uint32_t i = threadIdx.x; i < nn; i += kBlk) dst[(i / wn) * ws + i % wn] = sn[i];
+        for (uint32_t i = threadIdx.x; i < nn; i += kBlk) {
+            uint4 v = sn[i];
+            // BVH2 child codes (words 0 and 2: c0, c1) of internal nodes become slot offsets in
+            // 16-B units, so the traversal addresses a node with a shift (traced_bvh2's CUNIT)
+            if (TR == TR_BVH2_LDS && (i % wn) % 2u == 0u && v.w < OM_LEAF) v.w *= ws;
+            dst[(i / wn) * ws + i % wn] = v;
+        }
         uint32_t* ldst = (uint32_t*)(dst + nn / wn * ws);
         for (uint32_t i = threadIdx.x; i < S.n_b2leaves; i += kBlk) ldst[i] = S.b2leaves[i];
         __syncthreads();
@@ -287,7 +293,7 @@ __device__ __forceinline__ int trace(const OmSceneDev& S, const OmParamsDev& P, 
     else if (TR == TR_BVH4_GLOBAL)
         best = traced_bvh4<kBlk, Wk, true>(S, T.h4l, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w, T.h4g, T.nl);
     else if (TR == TR_BVH2_LDS)
-        best = traced_bvh2<kStackDepth, kBlk, Wk, false, OmBvh2Node, (int)kB2Stride>(S, T.b2n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
+        best = traced_bvh2<kStackDepth, kBlk, Wk, false, OmBvh2Node, 16>(S, T.b2n, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w);
     else if (TR == TR_BVH2_GLOBAL)
         best = traced_bvh2<kStackDepth, kBlk, Wk, true>(S, T.h2l, T.bl, T.recs, T.stk, o, d, P.tmin, closest, w, T.h2g, T.nl);
     else if (TR == TR_SBVH_GLOBAL) best = traced_sbvh(S, S.snodes, S.srecs, o, d, P.tmin, closest, w);

@@ -87,6 +87,7 @@ declare -A V=(
   # r06: BVH2 f32 LDS node stride (bank slots; default 80)
   [p64]="$COMMON $DEV -DOM_B2_NODE_STRIDE=64"
   [p96]="$COMMON $DEV -DOM_B2_NODE_STRIDE=96"
+  [p112]="$COMMON $DEV -DOM_B2_NODE_STRIDE=112"
   # LLVM AMDGPU scheduler strategies (same code, different instruction order)
   [ilp]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-ilp"
   [memclause]="$COMMON $DEV -mllvm -amdgpu-sched-strategy=max-memory-clause"
