@@ -16,14 +16,6 @@ template <int K> __device__ __forceinline__ float b2p(const OmBvh2Node& N) {
 // A half-precision box plane (OmBvh2NodeH) as f32, exactly.
 __device__ __forceinline__ float h2f(uint16_t b) { return (float)__builtin_bit_cast(_Float16, b); }
 template <int K> __device__ __forceinline__ float b2p(const OmBvh2NodeH& N) { return h2f(N.b[K]); }
-// A half node as its eight 32-bit words (the L2 tree's traversal merges a node read from LDS or
-// L2 as words: a merge of 16-bit fields costs a shift per field in both branches).
-struct OmBvh2NodeHW { uint32_t w[8]; };
-template <int K> __device__ __forceinline__ float b2p(const OmBvh2NodeHW& N) {
-    return h2f((uint16_t)(K % 2 ? N.w[K / 2] >> 16 : N.w[K / 2]));
-}
-__device__ __forceinline__ uint32_t b2c0(const OmBvh2NodeHW& N) { return N.w[6] & 0xFFFFu; }
-__device__ __forceinline__ uint32_t b2c1(const OmBvh2NodeHW& N) { return N.w[6] >> 16; }
 // Plane P (lox loy loz hix hiy hiz) of child k of a 4-wide node, f32 or half.
 template <int P> __device__ __forceinline__ float b4p(const OmBvh4Node& N, int k) {
     return P == 0 ? N.lox[k] : P == 1 ? N.loy[k] : P == 2 ? N.loz[k] : P == 3 ? N.hix[k] : P == 4 ? N.hiy[k] : N.hiz[k];
@@ -703,7 +695,7 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
     const float t_lo = tmin * 0.5f - 1e-3f;
     offer_always2(S, o, d, tmin, ix, iy, iz, nox, noy, noz, t_lo, closest, best, w);
     // slab tests of node N's two child boxes: -> h0, h1 (hit), and whether child 1 is nearer
-    auto slabs = [&](const auto& N, bool& h0, bool& h1, bool& swap) {
+    auto slabs = [&](const Node& N, bool& h0, bool& h1, bool& swap) {
         w.add_pre(2);
         const float t_hi = closest * 1.0001f + 1e-3f;
         // half planes (OmBvh2NodeH): the (float) conversion folds into v_fma_mix_f32
@@ -738,57 +730,18 @@ __device__ __forceinline__ int traced_bvh2(const OmSceneDev& S, const Node* node
             if (!pop()) break;
             continue;
         }
-        if constexpr (HYB && sizeof(Node) == sizeof(OmBvh2NodeHW)) {
-            // L2 tree (half nodes): two loads with explicit address spaces, merged as 32-bit words
-            // and the half planes taken from the words after the merge.  Written as one
-            // conditional load, the compiler selects the pointer and issues one flat load for LDS
-            // and L2 nodes (2% slower on C3); the LDS words are read as 8-B pieces, since loads of one
-            // width would be sunk into a flat load again.
-            OmBvh2NodeHW N;
-#if defined(__HIP_DEVICE_COMPILE__)
-            typedef const __attribute__((address_space(1))) uint4 G4;
-            typedef const __attribute__((address_space(3))) uint2 L2;
-#else
-            typedef const uint4 G4;                 // host pass: parsed only, never run
-            typedef const uint2 L2;
-#endif
-            if (cur >= nl) {
-                G4* g = (G4*)gnodes + cur * 2u;
-                const uint4 a = g[0], b = g[1];
-                N.w[0] = a.x; N.w[1] = a.y; N.w[2] = a.z; N.w[3] = a.w;
-                N.w[4] = b.x; N.w[5] = b.y; N.w[6] = b.z; N.w[7] = b.w;
-            } else {
-                L2* l = (L2*)nodes + cur * 4u;
-                const uint2 a = l[0], b = l[1], c = l[2], e = l[3];
-                N.w[0] = a.x; N.w[1] = a.y; N.w[2] = b.x; N.w[3] = b.y;
-                N.w[4] = c.x; N.w[5] = c.y; N.w[6] = e.x; N.w[7] = e.y;
-            }
-            bool h0, h1, swap;
-            slabs(N, h0, h1, swap);
-            if (h0 && h1) {
-                stk[sp * STRIDE] = (uint16_t)(swap ? b2c0(N) : b2c1(N));
-                ++sp;
-                cur = swap ? b2c1(N) : b2c0(N);
-            } else if (h0 || h1) {
-                cur = h0 ? b2c0(N) : b2c1(N);
-            } else {
-                if (!pop()) break;
-                continue;
-            }
+        const Node N = (HYB && cur >= nl) ? gnodes[cur] : *(const Node*)((const char*)nodes + cur * (uint32_t)CUNIT);
+        bool h0, h1, swap;
+        slabs(N, h0, h1, swap);
+        if (h0 && h1) {                             // near child next, far child pushed
+            stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1);   // sp < depth: om_upload_world sizes the stack
+            ++sp;
+            cur = swap ? N.c1 : N.c0;
+        } else if (h0 || h1) {
+            cur = h0 ? N.c0 : N.c1;
         } else {
-            const Node N = (HYB && cur >= nl) ? gnodes[cur] : *(const Node*)((const char*)nodes + cur * (uint32_t)CUNIT);
-            bool h0, h1, swap;
-            slabs(N, h0, h1, swap);
-            if (h0 && h1) {                             // near child next, far child pushed
-                stk[sp * STRIDE] = (uint16_t)(swap ? N.c0 : N.c1);   // sp < depth: om_upload_world sizes the stack
-                ++sp;
-                cur = swap ? N.c1 : N.c0;
-            } else if (h0 || h1) {
-                cur = h0 ? N.c0 : N.c1;
-            } else {
-                if (!pop()) break;
-                continue;
-            }
+            if (!pop()) break;
+            continue;
         }
     }
     return best;
